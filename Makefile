@@ -1,0 +1,37 @@
+# Build of the MI355X-native int8 path (hipcc only; no cmake needed).
+#   dlq_amd/libdlq.so  -- the C-ABI library (include/dlq.h)
+#   bin/dlq_e2e        -- the C++ launcher (reference infer_e2e.cu main)
+#   oracle/            -- the CPU checker (test infrastructure; oracle/Makefile)
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+# -ffp-contract=off: the fp32 epilogue/host-prep op order is part of the
+# numerics contract (every fused multiply-add is an explicit fmaf).
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result
+SRC = dlq_amd/csrc/kernels.hip dlq_amd/csrc/capi.cpp dlq_amd/csrc/resnet18.cpp dlq_amd/csrc/mlp.cpp
+HDR = include/dlq.h dlq_amd/csrc/dlq_internal.h
+
+all: dlq_amd/libdlq.so bin/dlq_e2e oracle
+
+build/%.o: dlq_amd/csrc/%.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+build/%.o: dlq_amd/csrc/%.cpp $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -x hip -c -o $@ $<
+
+dlq_amd/libdlq.so: build/kernels.o build/capi.o build/resnet18.o build/mlp.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+bin/dlq_e2e: dlq_amd/csrc/main_e2e.cpp dlq_amd/libdlq.so include/dlq.h
+	@mkdir -p bin
+	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -Ldlq_amd -ldlq -Wl,-rpath,'$$ORIGIN/../dlq_amd'
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build bin dlq_amd/libdlq.so
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

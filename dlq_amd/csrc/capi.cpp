@@ -1,0 +1,213 @@
+// capi.cpp -- the C ABI of include/dlq.h: argument checking, host-side weight
+// preparation (bit-identical op order to oracle/oracle.c) and the per-layer
+// operator entry points.  Errors are returned, never exit()ed (the reference's
+// CUDA_CHECK exits: CUDA/resnet18-kernel-lab/cpp/fp32/runtime/utils.hpp:23-32).
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/dlq.h"
+#include "dlq_internal.h"
+
+namespace dlq {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string& msg) { g_err = msg; }
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return DLQ_ERR_HIP;
+}
+
+static inline int sat_rne_host(float y) {
+  float q = std::rint(y);
+  q = q < -127.f ? -127.f : q;
+  q = q > 127.f ? 127.f : q;
+  return (int)q;
+}
+
+void quantize_weights(const float* w, int OC, int K, int8_t* q, float* scale) {
+  for (int o = 0; o < OC; ++o) {
+    float mx = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float a = std::fabs(w[(size_t)o * K + k]);
+      mx = a > mx ? a : mx;
+    }
+    const float s = mx > 0.f ? mx / 127.f : 1.f;
+    scale[o] = s;
+    for (int k = 0; k < K; ++k) q[(size_t)o * K + k] = (int8_t)sat_rne_host(w[(size_t)o * K + k] / s);
+  }
+}
+
+void fold_bn(float s_x, const float* s_w, const float* g, const float* b, const float* m,
+             const float* v, float eps, int OC, float* alpha, float* beta) {
+  for (int o = 0; o < OC; ++o) {
+    const float t = g[o] / std::sqrt(v[o] + eps);
+    const float sxw = s_x * s_w[o];
+    alpha[o] = sxw * t;
+    const float mt = m[o] * t;
+    beta[o] = b[o] - mt;
+  }
+}
+
+size_t packed_bytes(int OC, int C, int kH, int kW) {
+  if (OC <= 0 || C <= 0) return 0;
+  const size_t ocp = (size_t)packed_oc(OC);
+  if (is_stem(C, kH, kW)) return ocp * kStemK;
+  if (C % 64 != 0) return 0;
+  return ocp * (size_t)kH * kW * C;
+}
+
+void pack_conv_weights(const int8_t* q, int OC, int IC, int kH, int kW, int C, int8_t* out) {
+  const size_t total = packed_bytes(OC, C, kH, kW);
+  std::memset(out, 0, total);
+  const bool stem = is_stem(C, kH, kW);
+  const int kw_p = stem ? 8 : kW;                 // padded taps per row
+  const size_t K = stem ? (size_t)kStemK : (size_t)kH * kW * C;
+  for (int o = 0; o < OC; ++o)
+    for (int c = 0; c < IC; ++c)
+      for (int kh = 0; kh < kH; ++kh)
+        for (int kw = 0; kw < kW; ++kw)
+          out[(size_t)o * K + ((size_t)kh * kw_p + kw) * C + c] =
+              q[(((size_t)o * IC + c) * kH + kh) * kW + kw];
+}
+
+}  // namespace dlq
+
+using namespace dlq;
+
+extern "C" {
+
+const char* dlq_version(void) { return "dlq-mi355x 0.1.0 (gfx950, int8 MFMA)"; }
+const char* dlq_last_error(void) { return g_err.c_str(); }
+
+int dlq_device_arch(int dev, char* buf, int buflen) {
+  hipDeviceProp_t p;
+  hipError_t e = hipGetDeviceProperties(&p, dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+  std::snprintf(buf, (size_t)buflen, "%s", p.gcnArchName);
+  return DLQ_OK;
+}
+
+int dlq_quantize_weights_s8(const float* w, int OC, int K, int8_t* q, float* scale) {
+  if (!w || !q || !scale || OC <= 0 || K <= 0) return fail(DLQ_ERR_ARG, "quantize_weights: bad args");
+  quantize_weights(w, OC, K, q, scale);
+  return DLQ_OK;
+}
+
+int dlq_fold_bn(float s_x, const float* s_w, const float* g, const float* b, const float* m,
+                const float* v, float eps, int OC, float* alpha, float* beta) {
+  if (!s_w || !g || !b || !m || !v || !alpha || !beta || OC <= 0)
+    return fail(DLQ_ERR_ARG, "fold_bn: bad args");
+  fold_bn(s_x, s_w, g, b, m, v, eps, OC, alpha, beta);
+  return DLQ_OK;
+}
+
+int dlq_conv_packed_oc(int OC) { return OC > 0 ? packed_oc(OC) : 0; }
+
+size_t dlq_conv_packed_bytes(int OC, int C, int kH, int kW) { return packed_bytes(OC, C, kH, kW); }
+
+int dlq_pack_conv_weights_s8(const int8_t* q, int OC, int IC, int kH, int kW, int C, int8_t* packed) {
+  if (!q || !packed || IC > C || packed_bytes(OC, C, kH, kW) == 0)
+    return fail(DLQ_ERR_ARG, "pack_conv_weights: unsupported shape (need C%64==0 or the 7x7 C=4 stem)");
+  pack_conv_weights(q, OC, IC, kH, kW, C, packed);
+  return DLQ_OK;
+}
+
+int dlq_quantize_nchw_to_nhwc_s8(const float* x, int N, int C, int H, int W, int Cout, float inv_s,
+                                 int8_t* y, void* stream) {
+  if (!x || !y || N < 0 || C <= 0 || Cout < C || H <= 0 || W <= 0)
+    return fail(DLQ_ERR_ARG, "quantize_nchw_to_nhwc: bad args");
+  if (N == 0) return DLQ_OK;
+  hipError_t e = launch_quantize_nchw_to_nhwc(x, N, C, H, W, Cout, inv_s, y, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, hipGetErrorString(e));
+}
+
+int dlq_quantize_rows_s8(const float* x, int rows, int cols, int ldy, float inv_s, int8_t* y,
+                         void* stream) {
+  if (!x || !y || rows < 0 || cols <= 0 || ldy < cols || ldy % 4)
+    return fail(DLQ_ERR_ARG, "quantize_rows: bad args (ldy >= cols, ldy % 4 == 0)");
+  if (rows == 0) return DLQ_OK;
+  hipError_t e = launch_quantize_rows(x, rows, cols, ldy, inv_s, y, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, hipGetErrorString(e));
+}
+
+int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
+                       const float* alpha, const float* beta, const int8_t* residual,
+                       float res_scale, float inv_out_scale, int relu, int out_kind, void* y,
+                       void* stream) {
+  if (!d || !x || !w_packed || !y) return fail(DLQ_ERR_ARG, "conv2d: null pointer");
+  if (out_kind < 0 || out_kind > 2) return fail(DLQ_ERR_ARG, "conv2d: bad out_kind");
+  if (out_kind != DLQ_OUT_S32 && (!alpha || !beta)) return fail(DLQ_ERR_ARG, "conv2d: alpha/beta required");
+  if (d->N < 0 || d->H <= 0 || d->W <= 0 || d->OC <= 0 || d->kH <= 0 || d->kW <= 0 || d->sH <= 0 ||
+      d->sW <= 0 || d->pH < 0 || d->pW < 0)
+    return fail(DLQ_ERR_ARG, "conv2d: bad shape");
+  if (packed_bytes(d->OC, d->C, d->kH, d->kW) == 0)
+    return fail(DLQ_ERR_ARG, "conv2d: unsupported C (need C%64==0, or C==4 with a 7x7 kernel)");
+  ConvArgs a{};
+  a.x = x; a.w = w_packed; a.alpha = alpha; a.beta = beta; a.res = residual; a.y = y;
+  a.s_res = res_scale; a.inv_s = inv_out_scale;
+  a.N = d->N; a.H = d->H; a.W = d->W; a.C = d->C;
+  a.OH = out_dim(d->H, d->kH, d->sH, d->pH);
+  a.OW = out_dim(d->W, d->kW, d->sW, d->pW);
+  a.OC = d->OC; a.OCp = packed_oc(d->OC);
+  a.K = is_stem(d->C, d->kH, d->kW) ? kStemK : d->kH * d->kW * d->C;
+  a.kH = d->kH; a.kW = d->kW; a.sH = d->sH; a.sW = d->sW; a.pH = d->pH; a.pW = d->pW;
+  a.relu = relu ? 1 : 0; a.out_kind = out_kind;
+  if (a.OH <= 0 || a.OW <= 0) return fail(DLQ_ERR_ARG, "conv2d: empty output");
+  const long long P = (long long)a.N * a.OH * a.OW;
+  const long long in_bytes = (long long)a.N * a.H * a.W * a.C;
+  const long long out_bytes = P * a.OC * (out_kind == DLQ_OUT_S8 ? 1 : 4);
+  if (P >= (1LL << 31) || in_bytes >= (1LL << 31) || out_bytes >= (1LL << 31))
+    return fail(DLQ_ERR_ARG, "conv2d: tensor exceeds 2^31 bytes; split the batch");
+  if (out_kind == DLQ_OUT_S8 && a.OC % 4) return fail(DLQ_ERR_ARG, "conv2d: int8 output needs OC % 4 == 0");
+  if (residual && out_kind != DLQ_OUT_S8) return fail(DLQ_ERR_ARG, "conv2d: residual needs int8 output");
+  if (is_stem(a.C, a.kH, a.kW) && (residual || out_kind == DLQ_OUT_F32))
+    return fail(DLQ_ERR_ARG, "conv2d: stem supports int8 (no residual) or int32 output");
+  a.P = (int)P;
+  if (a.P == 0) return DLQ_OK;
+  hipError_t e = launch_conv(a, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d launch: ") + hipGetErrorString(e));
+}
+
+int dlq_linear_s8(const int8_t* x, int N, int K, const int8_t* w_packed, int OC, const float* alpha,
+                  const float* beta, float inv_out_scale, int relu, int out_kind, void* y,
+                  void* stream) {
+  if (K <= 0 || K % 64) return fail(DLQ_ERR_ARG, "linear: K must be a positive multiple of 64");
+  dlq_conv_desc d{N, 1, 1, K, OC, 1, 1, 1, 1, 0, 0};
+  return dlq_conv2d_nhwc_s8(&d, x, w_packed, alpha, beta, nullptr, 0.f, inv_out_scale, relu,
+                            out_kind, y, stream);
+}
+
+int dlq_maxpool2d_3x3_s2p1_nhwc_s8(const int8_t* x, int N, int C, int H, int W, int8_t* y,
+                                   void* stream) {
+  if (!x || !y || N < 0 || C <= 0 || C % 16 || H <= 0 || W <= 0)
+    return fail(DLQ_ERR_ARG, "maxpool: bad args (C % 16 == 0)");
+  if (N == 0) return DLQ_OK;
+  hipError_t e = launch_maxpool(x, N, C, H, W, y, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, hipGetErrorString(e));
+}
+
+int dlq_gap_nhwc_s8(const int8_t* x, int N, int C, int HW, float k, int8_t* y, void* stream) {
+  if (!x || !y || N < 0 || C <= 0 || C % 4 || HW <= 0) return fail(DLQ_ERR_ARG, "gap: bad args (C % 4 == 0)");
+  if (N == 0) return DLQ_OK;
+  hipError_t e = launch_gap(x, N, C, HW, k, y, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, hipGetErrorString(e));
+}
+
+int dlq_im2col_nchw_s8(const int8_t* x, int N, int C, int H, int W, int kH, int kW, int sH, int sW,
+                       int pH, int pW, int8_t* col, void* stream) {
+  if (!x || !col || N < 0 || C <= 0 || kH <= 0 || kW <= 0 || sH <= 0 || sW <= 0)
+    return fail(DLQ_ERR_ARG, "im2col: bad args");
+  if (out_dim(H, kH, sH, pH) <= 0 || out_dim(W, kW, sW, pW) <= 0) return fail(DLQ_ERR_ARG, "im2col: empty output");
+  if (N == 0) return DLQ_OK;
+  hipError_t e = launch_im2col_nchw(x, N, C, H, W, kH, kW, sH, sW, pH, pW, col, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, hipGetErrorString(e));
+}
+
+}  // extern "C"

@@ -1,0 +1,62 @@
+// dlq_internal.h -- shared declarations between the HIP kernels (kernels.hip)
+// and the host side (capi.cpp, resnet18.cpp, mlp.cpp).  Not installed.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+namespace dlq {
+
+// Conv launch parameters (device view).  Activations are NHWC int8.
+struct ConvArgs {
+  const int8_t* x;      // [N][H][W][C]
+  const int8_t* w;      // packed [OCp][K]
+  const float* alpha;   // [OCp]
+  const float* beta;    // [OCp]
+  const int8_t* res;    // [N][OH][OW][OC] or nullptr
+  void* y;              // [N][OH][OW][OC] (int8 / fp32 / int32)
+  float s_res;
+  float inv_s;
+  int N, H, W, C;
+  int OH, OW, OC, OCp, K;
+  int kH, kW, sH, sW, pH, pW;
+  int P;     // N*OH*OW
+  int relu;
+  int out_kind;
+};
+
+// Stem packing: C == 4, 7x7 taps padded to 8x8 -> K = 256.
+constexpr int kStemC = 4;
+constexpr int kStemK = 8 * 8 * 4;
+
+int packed_oc(int OC);
+bool is_stem(int C, int kH, int kW);
+
+// Kernel launchers (kernels.hip).  Return hipError_t of the launch.
+hipError_t launch_conv(const ConvArgs& a, hipStream_t s);
+hipError_t launch_quantize_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cout,
+                                        float inv_s, int8_t* y, hipStream_t s);
+hipError_t launch_quantize_rows(const float* x, int rows, int cols, int ldy, float inv_s,
+                                int8_t* y, hipStream_t s);
+hipError_t launch_maxpool(const int8_t* x, int N, int C, int H, int W, int8_t* y, hipStream_t s);
+hipError_t launch_gap(const int8_t* x, int N, int C, int HW, float k, int8_t* y, hipStream_t s);
+hipError_t launch_im2col_nchw(const int8_t* x, int N, int C, int H, int W, int kH, int kW, int sH,
+                              int sW, int pH, int pW, int8_t* col, hipStream_t s);
+
+// Thread-local error message (capi.cpp).
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+// Host weight preparation (capi.cpp), identical op order to oracle/oracle.c.
+void quantize_weights(const float* w, int OC, int K, int8_t* q, float* scale);
+void fold_bn(float s_x, const float* s_w, const float* g, const float* b, const float* m,
+             const float* v, float eps, int OC, float* alpha, float* beta);
+size_t packed_bytes(int OC, int C, int kH, int kW);
+void pack_conv_weights(const int8_t* q_oihw, int OC, int IC, int kH, int kW, int C,
+                       int8_t* packed);
+
+inline int out_dim(int in, int k, int s, int p) { return (in + 2 * p - k) / s + 1; }
+
+}  // namespace dlq

@@ -1,0 +1,123 @@
+// mlp.cpp -- int8 MNIST MLP forward behind dlq_mlp_* (include/dlq.h).
+//
+// Mirrors the forward half of CUDA/MNIST_on_GPU/v4.cu forward_timed
+// (:255-302: matmul_a_b_kernel -> bias_forward_kernel -> relu_forward_kernel
+// -> matmul_a_b_kernel -> bias_forward_kernel) and v5.cu forward_pass_only
+// (:127-157, cublasSgemm + bias_add_kernel + relu_kernel).  The softmax
+// (v4.cu:182-200) and the training half (backward, SGD) are out of scope.
+// Each layer is ONE launch of the int8 MFMA GEMM with bias, ReLU and the
+// requantisation fused into its epilogue; the reference issues three kernels
+// and a cudaDeviceSynchronize per op (v4.cu:260-265).
+#include <cstring>
+#include <vector>
+
+#include "../../include/dlq.h"
+#include "dlq_internal.h"
+
+using namespace dlq;
+
+struct dlq_mlp {
+  int in = 0, hidden = 0, out = 0, kp = 0, max_batch = 0;
+  float s_in = 1.f, s_hidden = 1.f;
+  int8_t* w1 = nullptr;  // packed [OCp(hidden)][kp]
+  int8_t* w2 = nullptr;  // packed [OCp(out)][hidden]
+  float *a1 = nullptr, *b1 = nullptr, *a2 = nullptr, *b2 = nullptr;
+  int8_t* xq = nullptr;  // [max_batch][kp]
+  int8_t* hq = nullptr;  // [max_batch][hidden]
+  std::vector<void*> allocs;
+};
+
+namespace {
+
+int up(dlq_mlp* m, void** dst, const void* src, size_t bytes) {
+  hipError_t e = hipMalloc(dst, bytes ? bytes : 16);
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc");
+  m->allocs.push_back(*dst);
+  if (src && bytes) {
+    e = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
+  }
+  return DLQ_OK;
+}
+
+// Reference layout W[in][out] (v4.cu:121-132) -> per-output-channel int8
+// rows, packed [OCp][kp]; alpha = s_x * s_w[o], beta = bias[o].
+int prep_layer(dlq_mlp* m, const float* Wt, const float* bias, int in, int out, int kp, float s_x,
+               int8_t** dw, float** da, float** db) {
+  std::vector<float> w((size_t)out * in);
+  for (int i = 0; i < in; ++i)
+    for (int o = 0; o < out; ++o) w[(size_t)o * in + i] = Wt[(size_t)i * out + o];
+  std::vector<int8_t> q(w.size());
+  std::vector<float> sw(out);
+  quantize_weights(w.data(), out, in, q.data(), sw.data());
+  std::vector<int8_t> packed(packed_bytes(out, kp, 1, 1));
+  pack_conv_weights(q.data(), out, in, 1, 1, kp, packed.data());
+  const int op = packed_oc(out);
+  std::vector<float> a(op, 0.f), b(op, 0.f);
+  for (int o = 0; o < out; ++o) {
+    a[o] = s_x * sw[o];
+    b[o] = bias[o];
+  }
+  int rc;
+  if ((rc = up(m, (void**)dw, packed.data(), packed.size())) || (rc = up(m, (void**)da, a.data(), op * 4)) ||
+      (rc = up(m, (void**)db, b.data(), op * 4)))
+    return rc;
+  return DLQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dlq_mlp_create(int in, int hidden, int out, const float* W1, const float* b1, const float* W2,
+                   const float* b2, float s_in, float s_hidden, int max_batch, void* stream,
+                   dlq_mlp** res) {
+  (void)stream;
+  if (!res || !W1 || !b1 || !W2 || !b2 || in <= 0 || hidden <= 0 || out <= 0 || max_batch <= 0)
+    return fail(DLQ_ERR_ARG, "mlp_create: bad args");
+  if (hidden % 64) return fail(DLQ_ERR_ARG, "mlp_create: hidden must be a multiple of 64");
+  if (!(s_in > 0.f) || !(s_hidden > 0.f)) return fail(DLQ_ERR_ARG, "mlp_create: scales must be > 0");
+  auto* m = new dlq_mlp();
+  m->in = in; m->hidden = hidden; m->out = out; m->kp = (in + 63) / 64 * 64;
+  m->max_batch = max_batch; m->s_in = s_in; m->s_hidden = s_hidden;
+  int rc;
+  if ((rc = prep_layer(m, W1, b1, in, hidden, m->kp, s_in, &m->w1, &m->a1, &m->b1)) ||
+      (rc = prep_layer(m, W2, b2, hidden, out, hidden, s_hidden, &m->w2, &m->a2, &m->b2)) ||
+      (rc = up(m, (void**)&m->xq, nullptr, (size_t)max_batch * m->kp)) ||
+      (rc = up(m, (void**)&m->hq, nullptr, (size_t)max_batch * hidden))) {
+    dlq_mlp_destroy(m);
+    return rc;
+  }
+  *res = m;
+  return DLQ_OK;
+}
+
+void dlq_mlp_destroy(dlq_mlp* m) {
+  if (!m) return;
+  for (void* p : m->allocs) (void)hipFree(p);
+  delete m;
+}
+
+int dlq_mlp_forward(dlq_mlp* m, const float* x, int B, float* logits, void* stream) {
+  if (!m) return fail(DLQ_ERR_ARG, "mlp_forward: null model");
+  if (B < 0 || B > m->max_batch) return fail(DLQ_ERR_ARG, "mlp_forward: batch exceeds max_batch");
+  if (B == 0) return DLQ_OK;
+  if (!x || !logits) return fail(DLQ_ERR_ARG, "mlp_forward: null argument");
+  int rc = dlq_quantize_rows_s8(x, B, m->in, m->kp, 1.0f / m->s_in, m->xq, stream);
+  if (rc) return rc;
+  rc = dlq_linear_s8(m->xq, B, m->kp, m->w1, m->hidden, m->a1, m->b1, 1.0f / m->s_hidden, 1,
+                     DLQ_OUT_S8, m->hq, stream);
+  if (rc) return rc;
+  return dlq_linear_s8(m->hq, B, m->hidden, m->w2, m->out, m->a2, m->b2, 1.f, 0, DLQ_OUT_F32,
+                       logits, stream);
+}
+
+int dlq_mlp_copy_hidden(const dlq_mlp* m, int B, int8_t* dst, size_t cap, void* stream) {
+  if (!m || !dst || B < 0 || B > m->max_batch) return fail(DLQ_ERR_ARG, "mlp_copy_hidden: bad args");
+  const size_t bytes = (size_t)B * m->hidden;
+  if (cap < bytes) return fail(DLQ_ERR_ARG, "mlp_copy_hidden: destination too small");
+  hipError_t e = hipMemcpyAsync(dst, m->hq, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : hip_fail(e, "mlp_copy_hidden");
+}
+
+}  // extern "C"

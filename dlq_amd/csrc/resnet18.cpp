@@ -1,0 +1,534 @@
+// resnet18.cpp -- the ResNet-18 int8 engine behind dlq_resnet18_* (include/dlq.h).
+//
+// Host-side mirror of the reference launcher
+// CUDA/resnet18-kernel-lab/cpp/fp32/runtime/infer_e2e.cu:
+//   conv2d_nhwc_s8      <- conv2d_nchw_im2col_gemm  (:102-136) + bn_launch (:83-97)
+//   basic_block_forward <- basic_block_forward       (:139-203, BlockParams :139-152)
+//   fc_forward          <- fc_forward                (:206-219)
+//   forward()           <- main()'s stage sequence   (:253-433)
+// Differences that are the point of the rebuild: weights are quantised,
+// BN-folded and uploaded ONCE (prepare), not re-read from disk and copied
+// H2D per call (:262, :304-334, :128); no cudaMalloc/cudaFree or host sync
+// inside forward (the reference frees temporaries per layer and syncs at
+// :280, :292, :423); the batch dimension is honoured; BN, ReLU, residual add
+// and requantisation run in the conv kernel's epilogue.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/dlq.h"
+#include "dlq_internal.h"
+
+using namespace dlq;
+
+namespace {
+
+struct ConvLayer {
+  std::string site;     // activation-scale site of this conv's OUTPUT, e.g. "layer1.0.conv1"
+  std::string wname;    // state_dict weight name
+  std::string bn;       // state_dict BN prefix
+  std::string in_site;  // scale site of the INPUT activation
+  int IC = 0, OC = 0, k = 0, s = 1, p = 0, Cstore = 0;
+  int8_t* w = nullptr;  // packed weights (device)
+  float* alpha = nullptr;
+  float* beta = nullptr;
+};
+
+struct Block {
+  std::string name;
+  int ic, oc, stride;
+  bool down;
+  int c1, c2, ds;  // indices into convs (ds = -1 if identity)
+};
+
+}  // namespace
+
+struct dlq_resnet18 {
+  std::map<std::string, std::vector<float>> tensors;
+  std::map<std::string, float> scales;
+  std::vector<ConvLayer> convs;
+  std::vector<Block> blocks;
+  int stem = -1;
+  // FC
+  int8_t* fc_w = nullptr;
+  float* fc_alpha = nullptr;
+  float* fc_beta = nullptr;
+  // workspace
+  int max_batch = 0;
+  int8_t* xq = nullptr;       // [B][224][224][4]
+  int8_t* c1 = nullptr;       // [B][112][112][64]
+  int8_t* buf[4] = {};        // block activations, each B*56*56*64 bytes
+  int8_t* gq = nullptr;       // [B][512]
+  std::vector<void*> allocs;
+  bool prepared = false;
+  // stage pointers of the last forward
+  std::map<std::string, std::pair<const int8_t*, size_t>> stage;
+  int last_B = 0;
+  // optional per-stage copies (parity dumps; infer_e2e.cu maybe_save :243-248)
+  bool keep = false;
+  std::map<std::string, int8_t*> keepbuf;
+  // optional conv-region timing: per forward 6 hipEvents bracketing
+  // [stem conv] [layer1.0.conv1 .. layer4.1.conv2] [fc]
+  bool timing = false;
+  std::vector<hipEvent_t> ev;
+  size_t ev_used = 0;
+};
+
+namespace {
+
+const int kBlocks[8][4] = {  // in, out, stride, downsample (infer_e2e.cu:336-407)
+    {64, 64, 1, 0},  {64, 64, 1, 0},  {64, 128, 2, 1},  {128, 128, 1, 0},
+    {128, 256, 2, 1}, {256, 256, 1, 0}, {256, 512, 2, 1}, {512, 512, 1, 0}};
+const char* kBlockNames[8] = {"layer1.0", "layer1.1", "layer2.0", "layer2.1",
+                              "layer3.0", "layer3.1", "layer4.0", "layer4.1"};
+
+void build_topology(dlq_resnet18* m) {
+  m->convs.clear();
+  m->blocks.clear();
+  ConvLayer st;
+  st.site = "conv1"; st.wname = "conv1.weight"; st.bn = "bn1"; st.in_site = "input";
+  st.IC = 3; st.OC = 64; st.k = 7; st.s = 2; st.p = 3; st.Cstore = kStemC;
+  m->convs.push_back(st);
+  m->stem = 0;
+  std::string prev = "conv1";
+  for (int b = 0; b < 8; ++b) {
+    const std::string n = kBlockNames[b];
+    Block blk{n, kBlocks[b][0], kBlocks[b][1], kBlocks[b][2], kBlocks[b][3] != 0, 0, 0, -1};
+    ConvLayer c1;
+    c1.site = n + ".conv1"; c1.wname = n + ".conv1.weight"; c1.bn = n + ".bn1"; c1.in_site = prev;
+    c1.IC = blk.ic; c1.OC = blk.oc; c1.k = 3; c1.s = blk.stride; c1.p = 1; c1.Cstore = blk.ic;
+    blk.c1 = (int)m->convs.size();
+    m->convs.push_back(c1);
+    if (blk.down) {
+      ConvLayer d;
+      d.site = n + ".downsample"; d.wname = n + ".downsample.0.weight"; d.bn = n + ".downsample.1";
+      d.in_site = prev;
+      d.IC = blk.ic; d.OC = blk.oc; d.k = 1; d.s = blk.stride; d.p = 0; d.Cstore = blk.ic;
+      blk.ds = (int)m->convs.size();
+      m->convs.push_back(d);
+    }
+    ConvLayer c2;
+    c2.site = n + ".conv2"; c2.wname = n + ".conv2.weight"; c2.bn = n + ".bn2"; c2.in_site = c1.site;
+    c2.IC = blk.oc; c2.OC = blk.oc; c2.k = 3; c2.s = 1; c2.p = 1; c2.Cstore = blk.oc;
+    blk.c2 = (int)m->convs.size();
+    m->convs.push_back(c2);
+    m->blocks.push_back(blk);
+    prev = c2.site;
+  }
+}
+
+std::vector<std::string> required_tensors(const dlq_resnet18* m) {
+  std::vector<std::string> r;
+  for (const auto& c : m->convs) {
+    r.push_back(c.wname);
+    for (const char* s : {".weight", ".bias", ".running_mean", ".running_var"}) r.push_back(c.bn + s);
+  }
+  r.push_back("fc.weight");
+  r.push_back("fc.bias");
+  return r;
+}
+
+size_t expected_numel(const dlq_resnet18* m, const std::string& name) {
+  for (const auto& c : m->convs) {
+    if (name == c.wname) return (size_t)c.OC * c.IC * c.k * c.k;
+    if (name.compare(0, c.bn.size() + 1, c.bn + ".") == 0) {
+      const std::string rest = name.substr(c.bn.size() + 1);
+      if (rest == "weight" || rest == "bias" || rest == "running_mean" || rest == "running_var")
+        return (size_t)c.OC;
+    }
+  }
+  if (name == "fc.weight") return 1000 * 512;
+  if (name == "fc.bias") return 1000;
+  return 0;
+}
+
+template <typename T>
+int dev_alloc(dlq_resnet18* m, T** p, size_t bytes) {
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, bytes ? bytes : 16);
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc");
+  m->allocs.push_back(q);
+  *p = (T*)q;
+  return DLQ_OK;
+}
+
+void free_all(dlq_resnet18* m) {
+  for (void* p : m->allocs) (void)hipFree(p);
+  m->allocs.clear();
+  for (auto& c : m->convs) { c.w = nullptr; c.alpha = nullptr; c.beta = nullptr; }
+  m->fc_w = nullptr; m->fc_alpha = m->fc_beta = nullptr;
+  m->xq = m->c1 = m->gq = nullptr;
+  for (auto& b : m->buf) b = nullptr;
+  m->keepbuf.clear();
+  m->prepared = false;
+}
+
+float inv_scale(float s) { return 1.0f / s; }
+
+// conv2d_nchw_im2col_gemm + bn_launch (+ add_inplace + relu_forward) of the
+// reference, as one implicit-GEMM launch with the epilogue fused.
+int conv2d_nhwc_s8(const dlq_resnet18* m, const ConvLayer& c, const int8_t* x, int N, int H, int W,
+                   const int8_t* residual, float res_scale, bool relu, int8_t* y, hipStream_t s,
+                   int* OH, int* OW) {
+  dlq_conv_desc d{N, H, W, c.Cstore, c.OC, c.k, c.k, c.s, c.s, c.p, c.p};
+  *OH = out_dim(H, c.k, c.s, c.p);
+  *OW = out_dim(W, c.k, c.s, c.p);
+  return dlq_conv2d_nhwc_s8(&d, x, c.w, c.alpha, c.beta, residual, res_scale,
+                            inv_scale(m->scales.at(c.site)), relu ? 1 : 0, DLQ_OUT_S8, y, s);
+}
+
+// basic_block_forward (infer_e2e.cu:156-203): conv-bn-relu, conv-bn,
+// identity | 1x1 downsample-bn, add, relu -- three launches at most.
+int basic_block_forward(const dlq_resnet18* m, const Block& b, const int8_t* in, int N, int H,
+                        int W, int8_t* h, int8_t* dsb, int8_t* out, hipStream_t s, int* OH,
+                        int* OW) {
+  int h1, w1, h2, w2;
+  int rc = conv2d_nhwc_s8(m, m->convs[b.c1], in, N, H, W, nullptr, 0.f, true, h, s, &h1, &w1);
+  if (rc) return rc;
+  const int8_t* skip = in;
+  float s_skip = m->scales.at(m->convs[b.c1].in_site);
+  if (b.down) {
+    int hd, wd;
+    rc = conv2d_nhwc_s8(m, m->convs[b.ds], in, N, H, W, nullptr, 0.f, false, dsb, s, &hd, &wd);
+    if (rc) return rc;
+    if (hd != h1 || wd != w1) return fail(DLQ_ERR_STATE, "downsample shape mismatch");
+    skip = dsb;
+    s_skip = m->scales.at(m->convs[b.ds].site);
+  }
+  rc = conv2d_nhwc_s8(m, m->convs[b.c2], h, N, h1, w1, skip, s_skip, true, out, s, &h2, &w2);
+  *OH = h2;
+  *OW = w2;
+  return rc;
+}
+
+// Record a stage output; with keep_stages on, snapshot it (the block ring
+// buffers are reused by later layers).
+int record_stage(dlq_resnet18* m, const char* name, const int8_t* p, size_t bytes, hipStream_t s) {
+  auto it = m->keepbuf.find(name);
+  if (m->keep && it != m->keepbuf.end()) {
+    hipError_t e = hipMemcpyAsync(it->second, p, bytes, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return hip_fail(e, "stage snapshot");
+    p = it->second;
+  }
+  m->stage[name] = {p, bytes};
+  return DLQ_OK;
+}
+
+int mark(dlq_resnet18* m, hipStream_t s) {
+  if (!m->timing) return DLQ_OK;
+  if (m->ev_used == m->ev.size()) {
+    if (m->ev.size() >= 6 * 8192) return fail(DLQ_ERR_STATE, "timing: event pool full; call dlq_resnet18_timing");
+    hipEvent_t e;
+    hipError_t he = hipEventCreate(&e);
+    if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
+    m->ev.push_back(e);
+  }
+  hipError_t he = hipEventRecord(m->ev[m->ev_used++], s);
+  return he == hipSuccess ? DLQ_OK : hip_fail(he, "hipEventRecord");
+}
+
+int check_ready(const dlq_resnet18* m) {
+  for (const auto& n : required_tensors(m))
+    if (!m->tensors.count(n)) return fail(DLQ_ERR_STATE, "missing tensor: " + n);
+  std::vector<std::string> sites = {"input", "gap"};
+  for (const auto& c : m->convs) sites.push_back(c.site);
+  for (const auto& s : sites)
+    if (!m->scales.count(s)) return fail(DLQ_ERR_STATE, "missing activation scale: " + s);
+  return DLQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dlq_resnet18_create(dlq_resnet18** out) {
+  if (!out) return fail(DLQ_ERR_ARG, "resnet18_create: null out");
+  auto* m = new dlq_resnet18();
+  build_topology(m);
+  *out = m;
+  return DLQ_OK;
+}
+
+void dlq_resnet18_destroy(dlq_resnet18* m) {
+  if (!m) return;
+  for (hipEvent_t e : m->ev) (void)hipEventDestroy(e);
+  free_all(m);
+  delete m;
+}
+
+int dlq_resnet18_set_tensor(dlq_resnet18* m, const char* name, const float* data, size_t n) {
+  if (!m || !name || !data) return fail(DLQ_ERR_ARG, "set_tensor: null argument");
+  const size_t want = expected_numel(m, name);
+  if (!want) return fail(DLQ_ERR_ARG, std::string("set_tensor: unknown tensor ") + name);
+  if (n != want)
+    return fail(DLQ_ERR_ARG, std::string("set_tensor: ") + name + " has " + std::to_string(n) +
+                                 " elements, expected " + std::to_string(want));
+  m->tensors[name].assign(data, data + n);
+  m->prepared = false;
+  return DLQ_OK;
+}
+
+int dlq_resnet18_set_scale(dlq_resnet18* m, const char* name, float scale) {
+  if (!m || !name) return fail(DLQ_ERR_ARG, "set_scale: null argument");
+  if (!(scale > 0.f) || !std::isfinite(scale)) return fail(DLQ_ERR_ARG, "set_scale: scale must be finite and > 0");
+  m->scales[name] = scale;
+  m->prepared = false;
+  return DLQ_OK;
+}
+
+// load_bin_f32 (utils.hpp:48-60) without the exit(): <dir>/<name>.bin.
+int dlq_resnet18_load_manifest(dlq_resnet18* m, const char* dir) {
+  if (!m || !dir) return fail(DLQ_ERR_ARG, "load_manifest: null argument");
+  for (const auto& n : required_tensors(m)) {
+    const std::string path = std::string(dir) + "/" + n + ".bin";
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return fail(DLQ_ERR_IO, "open fail: " + path);
+    f.seekg(0, std::ios::end);
+    const size_t bytes = (size_t)f.tellg();
+    f.seekg(0);
+    if (bytes % 4) return fail(DLQ_ERR_IO, "size not float-aligned: " + path);
+    std::vector<float> v(bytes / 4);
+    if (bytes) f.read((char*)v.data(), (std::streamsize)bytes);
+    if (!f) return fail(DLQ_ERR_IO, "read fail: " + path);
+    int rc = dlq_resnet18_set_tensor(m, n.c_str(), v.data(), v.size());
+    if (rc) return rc;
+  }
+  return DLQ_OK;
+}
+
+int dlq_resnet18_load_scales(dlq_resnet18* m, const char* path) {
+  if (!m || !path) return fail(DLQ_ERR_ARG, "load_scales: null argument");
+  std::ifstream f(path);
+  if (!f) return fail(DLQ_ERR_IO, std::string("open fail: ") + path);
+  std::string line;
+  while (std::getline(f, line)) {
+    if (line.empty() || line[0] == '#') continue;
+    std::istringstream ss(line);
+    std::string site;
+    float s;
+    if (!(ss >> site >> s)) return fail(DLQ_ERR_IO, "bad scale line: " + line);
+    int rc = dlq_resnet18_set_scale(m, site.c_str(), s);
+    if (rc) return rc;
+  }
+  return DLQ_OK;
+}
+
+int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
+  if (!m || max_batch <= 0) return fail(DLQ_ERR_ARG, "prepare: bad args");
+  int rc = check_ready(m);
+  if (rc) return rc;
+  free_all(m);
+  hipStream_t s = (hipStream_t)stream;
+  // Weights: quantise per output channel, fold BN, pack, upload once.
+  for (auto& c : m->convs) {
+    const std::vector<float>& w = m->tensors.at(c.wname);
+    const int K = c.IC * c.k * c.k;
+    const int ocp = packed_oc(c.OC);
+    std::vector<int8_t> q((size_t)c.OC * K);
+    std::vector<float> sw(c.OC);
+    quantize_weights(w.data(), c.OC, K, q.data(), sw.data());
+    const size_t pb = packed_bytes(c.OC, c.Cstore, c.k, c.k);
+    std::vector<int8_t> packed(pb);
+    pack_conv_weights(q.data(), c.OC, c.IC, c.k, c.k, c.Cstore, packed.data());
+    std::vector<float> alpha(ocp, 0.f), beta(ocp, 0.f);
+    fold_bn(m->scales.at(c.in_site), sw.data(), m->tensors.at(c.bn + ".weight").data(),
+            m->tensors.at(c.bn + ".bias").data(), m->tensors.at(c.bn + ".running_mean").data(),
+            m->tensors.at(c.bn + ".running_var").data(), 1e-5f, c.OC, alpha.data(), beta.data());
+    if ((rc = dev_alloc(m, &c.w, pb)) || (rc = dev_alloc(m, &c.alpha, ocp * 4)) ||
+        (rc = dev_alloc(m, &c.beta, ocp * 4)))
+      return rc;
+    hipError_t e;
+    if ((e = hipMemcpy(c.w, packed.data(), pb, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c.alpha, alpha.data(), ocp * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c.beta, beta.data(), ocp * 4, hipMemcpyHostToDevice)) != hipSuccess)
+      return hip_fail(e, "weight upload");
+  }
+  {  // FC: int8 [1000][512] per-row scales; logits = fmaf(acc, s_gap*s_w[o], bias[o])
+    const int O = 1000, I = 512, op = packed_oc(O);
+    std::vector<int8_t> q((size_t)O * I);
+    std::vector<float> sw(O);
+    quantize_weights(m->tensors.at("fc.weight").data(), O, I, q.data(), sw.data());
+    std::vector<int8_t> packed(packed_bytes(O, I, 1, 1));
+    pack_conv_weights(q.data(), O, I, 1, 1, I, packed.data());
+    std::vector<float> alpha(op, 0.f), beta(op, 0.f);
+    const float sg = m->scales.at("gap");
+    const std::vector<float>& bias = m->tensors.at("fc.bias");
+    for (int o = 0; o < O; ++o) {
+      alpha[o] = sg * sw[o];
+      beta[o] = bias[o];
+    }
+    if ((rc = dev_alloc(m, &m->fc_w, packed.size())) || (rc = dev_alloc(m, &m->fc_alpha, op * 4)) ||
+        (rc = dev_alloc(m, &m->fc_beta, op * 4)))
+      return rc;
+    hipError_t e;
+    if ((e = hipMemcpy(m->fc_w, packed.data(), packed.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(m->fc_alpha, alpha.data(), op * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(m->fc_beta, beta.data(), op * 4, hipMemcpyHostToDevice)) != hipSuccess)
+      return hip_fail(e, "fc upload");
+  }
+  // Workspace (int8 NHWC), sized once for max_batch.
+  const size_t B = (size_t)max_batch;
+  if ((rc = dev_alloc(m, &m->xq, B * 224 * 224 * kStemC)) ||
+      (rc = dev_alloc(m, &m->c1, B * 112 * 112 * 64)) || (rc = dev_alloc(m, &m->gq, B * 512)))
+    return rc;
+  for (auto& b : m->buf)
+    if ((rc = dev_alloc(m, &b, B * 56 * 56 * 64))) return rc;
+  if (m->keep) {
+    const std::pair<const char*, size_t> kb[] = {{"stem_pool", 56 * 56 * 64}, {"layer1", 56 * 56 * 64},
+                                                 {"layer2", 28 * 28 * 128}, {"layer3", 14 * 14 * 256},
+                                                 {"layer4", 7 * 7 * 512}};
+    for (const auto& k : kb) {
+      int8_t* p = nullptr;
+      if ((rc = dev_alloc(m, &p, B * k.second))) return rc;
+      m->keepbuf[k.first] = p;
+    }
+  }
+  (void)s;
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail(e, "prepare sync");
+  m->max_batch = max_batch;
+  m->prepared = true;
+  return DLQ_OK;
+}
+
+int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, void* stream) {
+  if (!m) return fail(DLQ_ERR_ARG, "forward: null model");
+  if (!m->prepared) return fail(DLQ_ERR_STATE, "forward: call dlq_resnet18_prepare first");
+  if (B < 0 || B > m->max_batch) return fail(DLQ_ERR_ARG, "forward: batch exceeds prepared max_batch");
+  if (B == 0) return DLQ_OK;  // empty batch: nothing to read or write
+  if (!x || !logits) return fail(DLQ_ERR_ARG, "forward: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t nB = (size_t)B;
+  int rc;
+  m->stage.clear();
+  // 0) input quantisation (fp32 NCHW -> int8 NHWC4)
+  rc = dlq_quantize_nchw_to_nhwc_s8(x, B, 3, 224, 224, kStemC, inv_scale(m->scales.at("input")), m->xq, stream);
+  if (rc) return rc;
+  m->stage["input_q"] = {m->xq, nB * 224 * 224 * kStemC};
+  // 1) stem conv 7x7/s2 + BN + ReLU (infer_e2e.cu:259-280)
+  int H, W;
+  if ((rc = mark(m, s))) return rc;
+  rc = conv2d_nhwc_s8(m, m->convs[m->stem], m->xq, B, 224, 224, nullptr, 0.f, true, m->c1, s, &H, &W);
+  if (rc) return rc;
+  if ((rc = mark(m, s))) return rc;
+  m->stage["conv1"] = {m->c1, nB * H * W * 64};
+  // maxpool 3x3/s2/p1 (:282-293)
+  int8_t* cur = m->buf[0];
+  rc = dlq_maxpool2d_3x3_s2p1_nhwc_s8(m->c1, B, 64, H, W, cur, stream);
+  if (rc) return rc;
+  H = out_dim(H, 3, 2, 1);
+  W = out_dim(W, 3, 2, 1);
+  if ((rc = record_stage(m, "stem_pool", cur, nB * H * W * 64, s))) return rc;
+  // 2-5) layer1..layer4 (:300-415)
+  if ((rc = mark(m, s))) return rc;
+  for (size_t bi = 0; bi < m->blocks.size(); ++bi) {
+    const Block& b = m->blocks[bi];
+    int8_t* fr[3];
+    int k = 0;
+    for (auto* p : m->buf)
+      if (p != cur && k < 3) fr[k++] = p;
+    int OH, OW;
+    rc = basic_block_forward(m, b, cur, B, H, W, fr[0], fr[1], fr[2], s, &OH, &OW);
+    if (rc) return rc;
+    cur = fr[2];
+    H = OH;
+    W = OW;
+    if (b.name.size() == 8 && b.name[7] == '1')
+      if ((rc = record_stage(m, b.name.substr(0, 6).c_str(), cur, nB * H * W * b.oc, s))) return rc;
+  }
+  if ((rc = mark(m, s))) return rc;
+  // 6) GAP + FC (:417-433)
+  const std::string last = m->convs[m->blocks.back().c2].site;
+  const float k = (m->scales.at(last) / (float)(H * W)) / m->scales.at("gap");
+  rc = dlq_gap_nhwc_s8(cur, B, 512, H * W, k, m->gq, stream);
+  if (rc) return rc;
+  m->stage["gap"] = {m->gq, nB * 512};
+  if ((rc = mark(m, s))) return rc;
+  rc = dlq_linear_s8(m->gq, B, 512, m->fc_w, 1000, m->fc_alpha, m->fc_beta, 1.f, 0, DLQ_OUT_F32,
+                     logits, stream);
+  if (rc) return rc;
+  if ((rc = mark(m, s))) return rc;
+  m->last_B = B;
+  return DLQ_OK;
+}
+
+int dlq_resnet18_set_timing(dlq_resnet18* m, int on) {
+  if (!m) return fail(DLQ_ERR_ARG, "set_timing: null");
+  m->timing = on != 0;
+  m->ev_used = 0;
+  return DLQ_OK;
+}
+
+int dlq_resnet18_timing(dlq_resnet18* m, double* conv_ms, int* forwards, int* conv_launches) {
+  if (!m) return fail(DLQ_ERR_ARG, "timing: null");
+  double total = 0;
+  const size_t n = m->ev_used / 6;
+  for (size_t f = 0; f < n; ++f) {
+    hipEvent_t* e = &m->ev[6 * f];
+    for (int r = 0; r < 3; ++r) {
+      hipError_t he = hipEventSynchronize(e[2 * r + 1]);
+      if (he != hipSuccess) return hip_fail(he, "hipEventSynchronize");
+      float ms = 0;
+      he = hipEventElapsedTime(&ms, e[2 * r], e[2 * r + 1]);
+      if (he != hipSuccess) return hip_fail(he, "hipEventElapsedTime");
+      total += ms;
+    }
+  }
+  if (conv_ms) *conv_ms = total;
+  if (forwards) *forwards = (int)n;
+  if (conv_launches) *conv_launches = (int)(n * (m->convs.size() + 1));
+  m->ev_used = 0;
+  return DLQ_OK;
+}
+
+int dlq_resnet18_set_keep_stages(dlq_resnet18* m, int on) {
+  if (!m) return fail(DLQ_ERR_ARG, "keep_stages: null");
+  if ((on != 0) != m->keep) m->prepared = false;
+  m->keep = on != 0;
+  return DLQ_OK;
+}
+
+int dlq_resnet18_stage(dlq_resnet18* m, const char* name, void* dst, size_t cap, size_t* bytes,
+                       void* stream) {
+  if (!m || !name) return fail(DLQ_ERR_ARG, "stage: null argument");
+  auto it = m->stage.find(name);
+  if (it == m->stage.end()) return fail(DLQ_ERR_STATE, std::string("stage: not available: ") + name);
+  if (bytes) *bytes = it->second.second;
+  if (!dst) return DLQ_OK;
+  if (cap < it->second.second) return fail(DLQ_ERR_ARG, "stage: destination too small");
+  hipError_t e = hipMemcpyAsync(dst, it->second.first, it->second.second, hipMemcpyDeviceToDevice,
+                                (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : hip_fail(e, "stage copy");
+}
+
+int dlq_resnet18_macs_per_image(const dlq_resnet18* m, double* conv_macs, double* fc_macs) {
+  if (!m) return fail(DLQ_ERR_ARG, "macs: null");
+  double cm = 0;
+  int H = 224;
+  // stem
+  {
+    const auto& c = m->convs[m->stem];
+    const int oh = out_dim(H, c.k, c.s, c.p);
+    cm += (double)c.OC * c.IC * c.k * c.k * oh * oh;
+    H = out_dim(oh, 3, 2, 1);
+  }
+  for (const auto& b : m->blocks) {
+    const auto& c1 = m->convs[b.c1];
+    const int oh = out_dim(H, c1.k, c1.s, c1.p);
+    cm += (double)c1.OC * c1.IC * 9 * oh * oh;
+    cm += (double)b.oc * b.oc * 9 * oh * oh;
+    if (b.down) cm += (double)b.oc * b.ic * oh * oh;
+    H = oh;
+  }
+  if (conv_macs) *conv_macs = cm;
+  if (fc_macs) *fc_macs = 1000.0 * 512.0;
+  return DLQ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,104 @@
+"""ctypes binding of libdlq.so (include/dlq.h).
+
+The product path: every call goes to the hand-written gfx950 kernels through
+the C ABI.  There is NO fallback -- if the library is missing or was not
+built, importing this module raises.  PyTorch is used only as plumbing
+(device memory, streams, torch.distributed); it is imported first so that
+libdlq.so binds to the same HIP runtime instance as torch (both load
+libamdhip64.so.7 by soname).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdlq.so")
+
+DLQ_OK = 0
+DLQ_OUT_S8, DLQ_OUT_F32, DLQ_OUT_S32 = 0, 1, 2
+
+
+class DLQError(RuntimeError):
+    pass
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ("N", "H", "W", "C", "OC", "kH", "kW", "sH", "sW", "pH", "pW")]
+
+
+_vp, _i, _f, _sz = C.c_void_p, C.c_int, C.c_float, C.c_size_t
+_SIGS = {
+    "dlq_version": ([], C.c_char_p),
+    "dlq_last_error": ([], C.c_char_p),
+    "dlq_device_arch": ([_i, C.c_char_p, _i], _i),
+    "dlq_quantize_weights_s8": ([_vp, _i, _i, _vp, _vp], _i),
+    "dlq_fold_bn": ([_f, _vp, _vp, _vp, _vp, _vp, _f, _i, _vp, _vp], _i),
+    "dlq_conv_packed_oc": ([_i], _i),
+    "dlq_conv_packed_bytes": ([_i, _i, _i, _i], _sz),
+    "dlq_pack_conv_weights_s8": ([_vp, _i, _i, _i, _i, _i, _vp], _i),
+    "dlq_quantize_nchw_to_nhwc_s8": ([_vp, _i, _i, _i, _i, _i, _f, _vp, _vp], _i),
+    "dlq_quantize_rows_s8": ([_vp, _i, _i, _i, _f, _vp, _vp], _i),
+    "dlq_conv2d_nhwc_s8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _i, _vp, _vp], _i),
+    "dlq_linear_s8": ([_vp, _i, _i, _vp, _i, _vp, _vp, _f, _i, _i, _vp, _vp], _i),
+    "dlq_maxpool2d_3x3_s2p1_nhwc_s8": ([_vp, _i, _i, _i, _i, _vp, _vp], _i),
+    "dlq_gap_nhwc_s8": ([_vp, _i, _i, _i, _f, _vp, _vp], _i),
+    "dlq_im2col_nchw_s8": ([_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp], _i),
+    "dlq_resnet18_create": ([C.POINTER(_vp)], _i),
+    "dlq_resnet18_destroy": ([_vp], None),
+    "dlq_resnet18_set_tensor": ([_vp, C.c_char_p, _vp, _sz], _i),
+    "dlq_resnet18_set_scale": ([_vp, C.c_char_p, _f], _i),
+    "dlq_resnet18_load_manifest": ([_vp, C.c_char_p], _i),
+    "dlq_resnet18_load_scales": ([_vp, C.c_char_p], _i),
+    "dlq_resnet18_set_keep_stages": ([_vp, _i], _i),
+    "dlq_resnet18_prepare": ([_vp, _i, _vp], _i),
+    "dlq_resnet18_forward": ([_vp, _vp, _i, _vp, _vp], _i),
+    "dlq_resnet18_stage": ([_vp, C.c_char_p, _vp, _sz, C.POINTER(_sz), _vp], _i),
+    "dlq_resnet18_set_timing": ([_vp, _i], _i),
+    "dlq_resnet18_timing": ([_vp, C.POINTER(C.c_double), C.POINTER(_i), C.POINTER(_i)], _i),
+    "dlq_resnet18_macs_per_image": ([_vp, C.POINTER(C.c_double), C.POINTER(C.c_double)], _i),
+    "dlq_mlp_create": ([_i, _i, _i, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, C.POINTER(_vp)], _i),
+    "dlq_mlp_destroy": ([_vp], None),
+    "dlq_mlp_forward": ([_vp, _vp, _i, _vp, _vp], _i),
+    "dlq_mlp_copy_hidden": ([_vp, _i, _vp, _sz, _vp], _i),
+}
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build()). "
+        "There is no fallback path.")
+lib = C.CDLL(LIB_PATH)
+for _name, (_args, _res) in _SIGS.items():
+    _fn = getattr(lib, _name)
+    _fn.argtypes = _args
+    _fn.restype = _res
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def last_error() -> str:
+    return lib.dlq_last_error().decode()
+
+
+def check(rc: int, what: str = "dlq") -> None:
+    if rc != DLQ_OK:
+        raise DLQError(f"{what} failed (code {rc}): {last_error()}")
+
+
+def ptr(t) -> int | None:
+    """Device (or host numpy) address of a tensor/array, None for None."""
+    if t is None:
+        return None
+    if isinstance(t, torch.Tensor):
+        return t.data_ptr()
+    return t.ctypes.data  # numpy
+
+
+def stream_handle(stream=None) -> int | None:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream

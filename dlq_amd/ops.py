@@ -1,0 +1,148 @@
+"""Per-layer int8 operators over the C ABI (torch tensors as device memory).
+
+Names follow the reference's per-layer call sites
+(CUDA/resnet18-kernel-lab/cpp/fp32/runtime/infer_e2e.cu and kernels/*.cu):
+``conv2d_nchw_im2col_gemm`` -> :func:`conv2d_nhwc_s8`,
+``maxpool2d_3x3_s2p1_nchw`` -> :func:`maxpool2d_3x3_s2p1_nhwc_s8`,
+``gap_global``              -> :func:`gap_nhwc_s8`,
+``fc_forward``              -> :func:`linear_s8`,
+``im2col_nchw``             -> :func:`im2col_nchw_s8` (parity only).
+Like the reference helpers they raise on failure instead of returning codes
+(the reference exits the process, utils.hpp:23-32).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from .lib import (DLQ_OUT_F32, DLQ_OUT_S8, DLQ_OUT_S32, ConvDesc, check, lib, ptr,
+                  stream_handle)
+
+
+def out_dim(n, k, s, p):
+    return (n + 2 * p - k) // s + 1
+
+
+# ------------------------------------------------------------------ host prep
+
+def quantize_weights(w: np.ndarray):
+    """Per-output-channel int8 weights (dlq_quantize_weights_s8): (q, scale)."""
+    w = np.ascontiguousarray(w, np.float32)
+    OC = w.shape[0]; K = w.size // OC
+    q = np.empty(w.shape, np.int8); s = np.empty(OC, np.float32)
+    check(lib.dlq_quantize_weights_s8(ptr(w), OC, K, ptr(q), ptr(s)), "quantize_weights")
+    return q, s
+
+
+def fold_bn(s_x: float, s_w, g, b, m, v, eps=1e-5):
+    arrs = [np.ascontiguousarray(a, np.float32) for a in (s_w, g, b, m, v)]
+    OC = arrs[1].size
+    alpha = np.empty(OC, np.float32); beta = np.empty(OC, np.float32)
+    check(lib.dlq_fold_bn(float(s_x), *[ptr(a) for a in arrs], float(eps), OC, ptr(alpha), ptr(beta)),
+          "fold_bn")
+    return alpha, beta
+
+
+def packed_oc(OC: int) -> int:
+    return lib.dlq_conv_packed_oc(OC)
+
+
+def pack_conv_weights(q_oihw: np.ndarray, C_store: int) -> np.ndarray:
+    q = np.ascontiguousarray(q_oihw, np.int8)
+    OC, IC, kH, kW = q.shape
+    nb = lib.dlq_conv_packed_bytes(OC, C_store, kH, kW)
+    if nb == 0:
+        raise ValueError(f"unsupported conv packing: C={C_store} k={kH}x{kW}")
+    out = np.empty(nb, np.int8)
+    check(lib.dlq_pack_conv_weights_s8(ptr(q), OC, IC, kH, kW, C_store, ptr(out)), "pack_conv_weights")
+    return out
+
+
+def pad_vec(v, n):
+    out = np.zeros(n, np.float32)
+    out[: len(v)] = v
+    return out
+
+
+# ------------------------------------------------------------------ device ops
+
+def _dev(t: torch.Tensor, dtype) -> None:
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == dtype and t.is_contiguous()):
+        raise TypeError(f"expected a contiguous CUDA tensor of {dtype}")
+
+
+def quantize_nchw_to_nhwc(x: torch.Tensor, scale: float, c_out: int = 4) -> torch.Tensor:
+    _dev(x, torch.float32)
+    N, Cc, H, W = x.shape
+    y = torch.empty((N, H, W, c_out), dtype=torch.int8, device=x.device)
+    inv = float(np.float32(1.0) / np.float32(scale))
+    check(lib.dlq_quantize_nchw_to_nhwc_s8(ptr(x), N, Cc, H, W, c_out, inv, ptr(y), stream_handle()),
+          "quantize_nchw_to_nhwc")
+    return y
+
+
+def quantize_rows(x: torch.Tensor, scale: float, ld: int) -> torch.Tensor:
+    _dev(x, torch.float32)
+    rows, cols = x.shape
+    y = torch.empty((rows, ld), dtype=torch.int8, device=x.device)
+    inv = float(np.float32(1.0) / np.float32(scale))
+    check(lib.dlq_quantize_rows_s8(ptr(x), rows, cols, ld, inv, ptr(y), stream_handle()), "quantize_rows")
+    return y
+
+
+def conv2d_nhwc_s8(x: torch.Tensor, w_packed: torch.Tensor, OC: int, k: int, stride: int, pad: int,
+                   alpha: torch.Tensor | None = None, beta: torch.Tensor | None = None,
+                   residual: torch.Tensor | None = None, res_scale: float = 0.0,
+                   out_scale: float = 1.0, relu: bool = True, out_kind: int = DLQ_OUT_S8):
+    """Implicit-GEMM int8 conv (+ fused epilogue) on NHWC x[N,H,W,C]."""
+    _dev(x, torch.int8)
+    N, H, W, Cc = x.shape
+    OH, OW = out_dim(H, k, stride, pad), out_dim(W, k, stride, pad)
+    dt = {DLQ_OUT_S8: torch.int8, DLQ_OUT_F32: torch.float32, DLQ_OUT_S32: torch.int32}[out_kind]
+    y = torch.empty((N, OH, OW, OC), dtype=dt, device=x.device)
+    d = ConvDesc(N, H, W, Cc, OC, k, k, stride, stride, pad, pad)
+    inv = float(np.float32(1.0) / np.float32(out_scale))
+    check(lib.dlq_conv2d_nhwc_s8(C.byref(d), ptr(x), ptr(w_packed), ptr(alpha), ptr(beta), ptr(residual),
+                                 float(res_scale), inv, int(relu), out_kind, ptr(y), stream_handle()),
+          "conv2d_nhwc_s8")
+    return y
+
+
+def linear_s8(x: torch.Tensor, w_packed: torch.Tensor, OC: int, alpha=None, beta=None,
+              out_scale: float = 1.0, relu: bool = False, out_kind: int = DLQ_OUT_F32):
+    _dev(x, torch.int8)
+    N, K = x.shape
+    dt = {DLQ_OUT_S8: torch.int8, DLQ_OUT_F32: torch.float32, DLQ_OUT_S32: torch.int32}[out_kind]
+    y = torch.empty((N, OC), dtype=dt, device=x.device)
+    inv = float(np.float32(1.0) / np.float32(out_scale))
+    check(lib.dlq_linear_s8(ptr(x), N, K, ptr(w_packed), OC, ptr(alpha), ptr(beta), inv, int(relu),
+                            out_kind, ptr(y), stream_handle()), "linear_s8")
+    return y
+
+
+def maxpool2d_3x3_s2p1_nhwc_s8(x: torch.Tensor) -> torch.Tensor:
+    _dev(x, torch.int8)
+    N, H, W, Cc = x.shape
+    y = torch.empty((N, out_dim(H, 3, 2, 1), out_dim(W, 3, 2, 1), Cc), dtype=torch.int8, device=x.device)
+    check(lib.dlq_maxpool2d_3x3_s2p1_nhwc_s8(ptr(x), N, Cc, H, W, ptr(y), stream_handle()), "maxpool")
+    return y
+
+
+def gap_nhwc_s8(x: torch.Tensor, k: float) -> torch.Tensor:
+    _dev(x, torch.int8)
+    N, H, W, Cc = x.shape
+    y = torch.empty((N, Cc), dtype=torch.int8, device=x.device)
+    check(lib.dlq_gap_nhwc_s8(ptr(x), N, Cc, H * W, float(k), ptr(y), stream_handle()), "gap")
+    return y
+
+
+def im2col_nchw_s8(x: torch.Tensor, k: int, stride: int, pad: int) -> torch.Tensor:
+    _dev(x, torch.int8)
+    N, Cc, H, W = x.shape
+    OH, OW = out_dim(H, k, stride, pad), out_dim(W, k, stride, pad)
+    col = torch.empty((N, Cc * k * k, OH * OW), dtype=torch.int8, device=x.device)
+    check(lib.dlq_im2col_nchw_s8(ptr(x), N, Cc, H, W, k, k, stride, stride, pad, pad, ptr(col),
+                                 stream_handle()), "im2col")
+    return col

@@ -1,0 +1,203 @@
+/*
+ * dlq.h -- C ABI of the MI355X-native int8 CNN inference path (libdlq.so).
+ *
+ * Drop-in for the conv/GEMM inference path of yeontachi/DLQ:
+ *   CUDA/resnet18-kernel-lab/cpp/fp32/{kernels,runtime}  (ResNet-18)
+ *   CUDA/MNIST_on_GPU/v4.cu, v5.cu                      (MLP FC GEMM, forward)
+ * Every entry point below names the reference interface it replaces
+ * (file:line, relative to the reference repository root; "RK" abbreviates
+ * CUDA/resnet18-kernel-lab/cpp/fp32).
+ *
+ * Conventions (differences from the reference are deliberate):
+ *   - plain C types only; device pointers are HIP device addresses; `stream`
+ *     is a hipStream_t (NULL = the legacy default stream, as in the reference);
+ *   - every call returns an int status (DLQ_OK = 0) and NEVER exits the
+ *     process (the reference's CUDA_CHECK calls std::exit(1), RK/runtime/
+ *     utils.hpp:23-32); dlq_last_error() gives the message of the last failure
+ *     on the calling thread;
+ *   - the batch dimension N is honoured everywhere (the reference hard-wires
+ *     N=1, RK/kernels/im2col.cu:11-12);
+ *   - activations are int8 NHWC on the device ("channels-last", the layout the
+ *     int8 MFMA contraction wants); NCHW survives at the boundaries: the fp32
+ *     input is NCHW (as RK/runtime/infer_e2e.cu:254-256), and
+ *     dlq_im2col_nchw_s8 / stage dumps use NCHW.
+ * No call allocates or synchronises unless documented (the create / prepare
+ * calls do), so forward calls can be captured into a hipGraph.
+ */
+#ifndef DLQ_H
+#define DLQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DLQ_OK 0
+#define DLQ_ERR_ARG 1    /* bad shape / pointer / unsupported configuration      */
+#define DLQ_ERR_HIP 2    /* HIP runtime error (utils.hpp:23-32 analogue)          */
+#define DLQ_ERR_LAUNCH 3 /* kernel launch failed (utils.hpp:34-45 returns 3)     */
+#define DLQ_ERR_IO 4     /* file I/O (utils.hpp:48-67 analogue)                   */
+#define DLQ_ERR_STATE 5  /* object used before prepare / missing tensor or scale */
+
+/* Epilogue output kinds of dlq_conv2d_nhwc_s8 / dlq_linear_s8. */
+#define DLQ_OUT_S8 0  /* requantised int8 (fused BN/bias, residual, ReLU)         */
+#define DLQ_OUT_F32 1 /* fp32 = fmaf(float(acc), alpha, beta) (dequant / logits) */
+#define DLQ_OUT_S32 2 /* raw int32 accumulators (parity / debugging)             */
+
+const char* dlq_version(void);
+const char* dlq_last_error(void);
+/* Name of HIP device `dev` (e.g. "gfx950"); DLQ_ERR_HIP without a GPU. */
+int dlq_device_arch(int dev, char* buf, int buflen);
+
+/* ------------------------------------------------------------------------ */
+/* Host-side weight preparation (no device, deterministic, bit-identical to */
+/* the CPU oracle).  The reference copies fp32 OIHW weights as-is           */
+/* (RK/runtime/infer_e2e.cu:114-126 is an identity repack).                 */
+/* ------------------------------------------------------------------------ */
+
+/* Symmetric per-output-channel quantisation of w[OC][K]:
+ * scale[o] = max|w[o,:]|/127 (1 if all zero), q = clamp(rne(w/scale), +-127). */
+int dlq_quantize_weights_s8(const float* w, int OC, int K, int8_t* q, float* scale);
+
+/* Dequant * BatchNorm folded into one affine per channel (replaces bn_launch,
+ * RK/runtime/infer_e2e.cu:83-97 and RK/kernels/bn_inference.cu:22-27):
+ *   t = g/sqrtf(v+eps); alpha = (s_x*s_w)*t; beta = b - m*t.                 */
+int dlq_fold_bn(float s_x, const float* s_w, const float* g, const float* b, const float* m,
+                const float* v, float eps, int OC, float* alpha, float* beta);
+
+/* Padded output-channel count the packed weights / alpha / beta must have. */
+int dlq_conv_packed_oc(int OC);
+/* Bytes of the packed weight image for a conv over NHWC input with C stored
+ * channels.  Supported: C % 64 == 0 (any kH,kW), or the stem (C == 4,
+ * kH == kW == 7).  Returns 0 for unsupported shapes. */
+size_t dlq_conv_packed_bytes(int OC, int C, int kH, int kW);
+/* Pack int8 OIHW weights q[OC][IC][kH][kW] (IC <= C; channels IC..C-1 and
+ * padded rows are zero) into the kernel's [OCp][K] image. */
+int dlq_pack_conv_weights_s8(const int8_t* q_oihw, int OC, int IC, int kH, int kW, int C,
+                             int8_t* packed);
+
+/* ------------------------------------------------------------------------ */
+/* Device operators (per-layer entry points; all asynchronous on `stream`)  */
+/* ------------------------------------------------------------------------ */
+
+typedef struct dlq_conv_desc {
+  int N, H, W, C; /* input NHWC; C = stored channels (4 for the RGB stem)     */
+  int OC;         /* output channels                                          */
+  int kH, kW, sH, sW, pH, pW;
+} dlq_conv_desc;
+
+/* Input quantisation (new; the reference feeds fp32 straight to im2col,
+ * RK/runtime/infer_e2e.cu:255-256): fp32 NCHW x[N][C][H][W] ->
+ * int8 NHWC y[N][H][W][Cout], channels C..Cout-1 zero; q = clamp(rne(x*inv_s)). */
+int dlq_quantize_nchw_to_nhwc_s8(const float* x, int N, int C, int H, int W, int Cout, float inv_s,
+                                 int8_t* y, void* stream);
+/* Row quantisation fp32 x[rows][cols] -> int8 y[rows][ldy] (zero padded). */
+int dlq_quantize_rows_s8(const float* x, int rows, int cols, int ldy, float inv_s, int8_t* y,
+                         void* stream);
+
+/* Implicit-im2col int8 conv + fused epilogue.  Replaces
+ * conv2d_nchw_im2col_gemm (RK/runtime/infer_e2e.cu:102-136: im2col_nchw +
+ * sgemm_tiled) followed by bn_launch (:83-97), add_inplace (RK/kernels/add.cu)
+ * and relu_forward (RK/kernels/relu.cu) as wired in basic_block_forward
+ * (:156-203).  Output NHWC [N][OH][OW][OC]:
+ *   DLQ_OUT_S8 : y = fmaf(float(acc), alpha[o], beta[o]);
+ *                y = fmaf(float(residual), res_scale, y) if residual != NULL;
+ *                y = max(y, 0) if relu; out = clamp(rne(y * inv_out_scale), +-127)
+ *   DLQ_OUT_F32: out = fmaf(float(acc), alpha[o], beta[o]) (max(.,0) if relu)
+ *   DLQ_OUT_S32: out = acc (int32)                                           */
+int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
+                       const float* alpha, const float* beta, const int8_t* residual,
+                       float res_scale, float inv_out_scale, int relu, int out_kind, void* y,
+                       void* stream);
+
+/* Dense layer on int8 rows: y[N][OC] from x[N][K] (K % 64 == 0) and packed
+ * weights [OCp][K]; same epilogue kinds.  Replaces fc_forward
+ * (RK/runtime/infer_e2e.cu:206-219: sgemm_tiled M=1000,N=1,K=512 + host bias)
+ * and the MNIST forward GEMMs (CUDA/MNIST_on_GPU/v4.cu:255-302
+ * matmul_a_b_kernel + bias_forward_kernel + relu_forward_kernel;
+ * v5.cu:127-157 cublasSgemm + bias_add_kernel + relu_kernel). */
+int dlq_linear_s8(const int8_t* x, int N, int K, const int8_t* w_packed, int OC, const float* alpha,
+                  const float* beta, float inv_out_scale, int relu, int out_kind, void* y,
+                  void* stream);
+
+/* 3x3/s2/p1 max pool on int8 NHWC (RK/kernels/maxpool2d.cu:4-41, launched at
+ * RK/runtime/infer_e2e.cu:283-293; out-of-bounds taps skipped). */
+int dlq_maxpool2d_3x3_s2p1_nhwc_s8(const int8_t* x, int N, int C, int H, int W, int8_t* y,
+                                   void* stream);
+
+/* Global average pool (gap_global_ref, RK/runtime/infer_e2e.cu:37-61;
+ * RK/kernels/gap_global.cu) on int8 NHWC [N][HW][C] -> int8 [N][C]:
+ * exact int32 sum, then clamp(rne(float(sum) * k)), k = s_in/HW/s_out. */
+int dlq_gap_nhwc_s8(const int8_t* x, int N, int C, int HW, float k, int8_t* y, void* stream);
+
+/* im2col in the reference's row order r = c*kH*kW + kh*kW + kw
+ * (RK/kernels/im2col.cu:5-58) on int8 NCHW, batch honoured: col[N][K][OH*OW].
+ * Parity/debug only -- the conv kernel gathers patches implicitly. */
+int dlq_im2col_nchw_s8(const int8_t* x, int N, int C, int H, int W, int kH, int kW, int sH, int sW,
+                       int pH, int pW, int8_t* col, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* ResNet-18 engine: the launcher's per-layer sequence (RK/runtime/         */
+/* infer_e2e.cu:259-438) with weights resident and a preallocated workspace */
+/* ------------------------------------------------------------------------ */
+typedef struct dlq_resnet18 dlq_resnet18;
+
+int dlq_resnet18_create(dlq_resnet18** out);
+void dlq_resnet18_destroy(dlq_resnet18* m);
+/* fp32 tensor by torch state_dict name, e.g. "layer1.0.conv1.weight",
+ * "bn1.running_var", "fc.bias" (the export format of
+ * tools/export_resnet18.py:85-104; the loader of infer_e2e.cu:226-228). */
+int dlq_resnet18_set_tensor(dlq_resnet18* m, const char* name, const float* data, size_t n);
+/* Activation scale (fp32, > 0) by site: "input", "conv1",
+ * "layerX.Y.conv1", "layerX.Y.conv2", "layerX.0.downsample", "gap". */
+int dlq_resnet18_set_scale(dlq_resnet18* m, const char* name, float scale);
+/* Read every tensor from <dir>/<name>.bin (the reference's manifest dir,
+ * RK/runtime/infer_e2e.cu:262-334,428-429). */
+int dlq_resnet18_load_manifest(dlq_resnet18* m, const char* dir);
+/* Read "<site> <scale>" lines (the int8 quant block). */
+int dlq_resnet18_load_scales(dlq_resnet18* m, const char* path);
+/* Quantise + fold + upload weights, allocate the workspace for up to
+ * max_batch images.  Synchronous. */
+int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream);
+/* logits[B][1000] fp32 (device) from x[B][3][224][224] fp32 NCHW (device). */
+int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, void* stream);
+/* Keep snapshots of every stage output (for dumps/parity; costs D2D copies
+ * inside forward).  Takes effect at the next dlq_resnet18_prepare. */
+int dlq_resnet18_set_keep_stages(dlq_resnet18* m, int on);
+/* Copy a stage activation of the last forward to device memory `dst`:
+ * "input_q", "conv1", "stem_pool", "layer1".."layer4" (int8 NHWC) or
+ * "gap" (int8 [B][512]).  *bytes receives the size. */
+int dlq_resnet18_stage(dlq_resnet18* m, const char* name, void* dst, size_t cap, size_t* bytes,
+                       void* stream);
+/* Conv-kernel timing: with timing on, every forward records hipEvents on its
+ * stream around the stem conv, the 19 block convs (layer1.0.conv1 ..
+ * layer4.1.conv2, nothing else launched in between) and the FC GEMM.
+ * dlq_resnet18_timing synchronises on them, returns the summed milliseconds,
+ * the forwards and conv-kernel launches covered, and resets the counters. */
+int dlq_resnet18_set_timing(dlq_resnet18* m, int on);
+int dlq_resnet18_timing(dlq_resnet18* m, double* conv_ms, int* forwards, int* conv_launches);
+/* Algorithmic MACs per image of the 20 convs and of the FC layer. */
+int dlq_resnet18_macs_per_image(const dlq_resnet18* m, double* conv_macs, double* fc_macs);
+
+/* ------------------------------------------------------------------------ */
+/* MNIST MLP (CUDA/MNIST_on_GPU/v4.cu forward_timed :255-302, v5.cu        */
+/* forward_pass_only :127-157): in -> hidden (ReLU) -> out, int8.           */
+/* ------------------------------------------------------------------------ */
+typedef struct dlq_mlp dlq_mlp;
+/* W1[in][hidden], W2[hidden][out] in the reference's [in][out] layout
+ * (v4.cu:121-132 computes X[B][in] @ W[in][out]). */
+int dlq_mlp_create(int in, int hidden, int out, const float* W1, const float* b1, const float* W2,
+                   const float* b2, float s_in, float s_hidden, int max_batch, void* stream,
+                   dlq_mlp** m);
+void dlq_mlp_destroy(dlq_mlp* m);
+int dlq_mlp_forward(dlq_mlp* m, const float* x, int B, float* logits, void* stream);
+/* Copy the int8 hidden activations [B][hidden] of the last forward (device
+ * to device, async on `stream`); cap = bytes available at dst. */
+int dlq_mlp_copy_hidden(const dlq_mlp* m, int B, int8_t* dst, size_t cap, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DLQ_H */

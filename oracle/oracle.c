@@ -1,0 +1,357 @@
+/*
+ * oracle.c -- CPU restatement of the yeontachi/DLQ ResNet-18 / MNIST-FC hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the checker, never the product:
+ * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load it.  The shipped path (libdlq.so) never links or calls anything here.
+ *
+ * Two families of functions:
+ *   ora_*_f32  -- the reference's fp32 semantics, op for op.  The reference
+ *                 GPU build contracts `acc += a*b` to FMA (nvcc -fmad=true,
+ *                 cpp/CMakeLists.txt:7-8 sets no flags), so every GEMM here
+ *                 is a k-ordered fmaf chain.  Pinned bit-exactly by the
+ *                 reference's own golden vector out/step8_logits.bin
+ *                 (tests/test_oracle.py).
+ *   ora_*_s8   -- the int8 path.  The reference has NO int8 code (SURVEY.md
+ *                 §0.1); the scheme is the build's own and this
+ *                 file is its definition.  Integer parts are exact; the fp32
+ *                 epilogue is a fixed sequence of IEEE ops (explicit fmaf,
+ *                 rintf = round-half-even) that the HIP kernels repeat.
+ *
+ * Build: oracle/Makefile (gcc -O3 -ffp-contract=off).  Layouts are the
+ * reference's: NCHW activations, OIHW weights, per-image im2col rows ordered
+ * r = c*kH*kW + kh*kW + kw (kernels/im2col.cu:37-54).
+ */
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORA_API __attribute__((visibility("default")))
+
+static inline int out_dim(int in, int k, int s, int p) { return (in + 2 * p - k) / s + 1; }
+
+/* ------------------------------------------------------------------ */
+/* fp32 reference semantics                                            */
+/* ------------------------------------------------------------------ */
+
+/* kernels/im2col.cu:5-58 -- one image; col[r][oh*OW+ow], zero padding. */
+ORA_API void ora_im2col_nchw_f32(const float* x, int C, int H, int W, int kH, int kW, int sH,
+                                 int sW, int pH, int pW, float* col) {
+  const int OH = out_dim(H, kH, sH, pH), OW = out_dim(W, kW, sW, pW);
+  const int cs = OH * OW;
+  for (int c = 0; c < C; ++c)
+    for (int kh = 0; kh < kH; ++kh)
+      for (int kw = 0; kw < kW; ++kw) {
+        const int r = c * kH * kW + kh * kW + kw;
+        for (int oh = 0; oh < OH; ++oh)
+          for (int ow = 0; ow < OW; ++ow) {
+            const int ih = oh * sH - pH + kh, iw = ow * sW - pW + kw;
+            float v = 0.f;
+            if (ih >= 0 && iw >= 0 && ih < H && iw < W) v = x[(size_t)c * H * W + ih * W + iw];
+            col[(size_t)r * cs + oh * OW + ow] = v;
+          }
+      }
+}
+
+/* kernels/sgemm_tiled.cu:22-45 -- C[M][N] = A[M][K] * B[K][N], row-major.
+ * Each output is acc = fmaf(A[m][k], B[k][n], acc) for k = 0..K-1 in order
+ * (the contracted form of `acc += As*Bs`, sgemm_tiled.cu:36).  The loop is
+ * k-outer/n-inner so it vectorises while keeping every element's k order. */
+ORA_API void ora_sgemm_f32(const float* A, const float* B, float* C, int M, int N, int K) {
+  for (int m = 0; m < M; ++m) {
+    float* c = C + (size_t)m * N;
+    for (int n = 0; n < N; ++n) c[n] = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float a = A[(size_t)m * K + k];
+      const float* b = B + (size_t)k * N;
+      for (int n = 0; n < N; ++n) c[n] = fmaf(a, b[n], c[n]);
+    }
+  }
+}
+
+/* kernels/bn_inference.cu:22-27 -- in place, x laid out [C][HW]. */
+ORA_API void ora_bn_inference_f32(float* x, const float* g, const float* b, const float* m,
+                                  const float* v, float eps, int C, int HW) {
+  for (int c = 0; c < C; ++c) {
+    const float d = sqrtf(v[c] + eps);
+    for (int i = 0; i < HW; ++i) {
+      const float y = (x[(size_t)c * HW + i] - m[c]) / d;
+      x[(size_t)c * HW + i] = fmaf(g[c], y, b[c]);
+    }
+  }
+}
+
+/* kernels/relu.cu:9 */
+ORA_API void ora_relu_f32(float* x, int n) {
+  for (int i = 0; i < n; ++i)
+    if (x[i] < 0.f) x[i] = 0.f;
+}
+
+/* kernels/add.cu:7 */
+ORA_API void ora_add_f32(float* y, const float* x, int n) {
+  for (int i = 0; i < n; ++i) y[i] += x[i];
+}
+
+/* kernels/maxpool2d.cu:14-40 -- 3x3/s2/p1, out-of-bounds taps skipped. */
+ORA_API void ora_maxpool_f32(const float* x, int N, int C, int H, int W, float* y) {
+  const int OH = out_dim(H, 3, 2, 1), OW = out_dim(W, 3, 2, 1);
+  for (int nc = 0; nc < N * C; ++nc)
+    for (int oh = 0; oh < OH; ++oh)
+      for (int ow = 0; ow < OW; ++ow) {
+        float vmax = -FLT_MAX;
+        for (int kh = 0; kh < 3; ++kh) {
+          const int ih = oh * 2 - 1 + kh;
+          if (ih < 0 || ih >= H) continue;
+          for (int kw = 0; kw < 3; ++kw) {
+            const int iw = ow * 2 - 1 + kw;
+            if (iw < 0 || iw >= W) continue;
+            const float v = x[(size_t)nc * H * W + ih * W + iw];
+            vmax = v > vmax ? v : vmax;
+          }
+        }
+        y[(size_t)nc * OH * OW + oh * OW + ow] = vmax;
+      }
+}
+
+/* runtime/infer_e2e.cu:37-61 (gap_global_ref; kernels/gap_global.cu has the
+ * same order): 256 strided partial sums, then a tree over strides 128..1. */
+ORA_API void ora_gap_f32(const float* x, int C, int HW, float* y) {
+  float s[256];
+  for (int c = 0; c < C; ++c) {
+    for (int t = 0; t < 256; ++t) {
+      float acc = 0.f;
+      for (int i = t; i < HW; i += 256) acc += x[(size_t)c * HW + i];
+      s[t] = acc;
+    }
+    for (int st = 128; st > 0; st >>= 1)
+      for (int t = 0; t < st; ++t) s[t] += s[t + st];
+    y[c] = s[0] / (float)HW;
+  }
+}
+
+/* runtime/infer_e2e.cu:206-219 -- GEMM W[O][I] * gap[I] (N=1) then a host
+ * fp32 bias add. */
+ORA_API void ora_fc_forward_f32(const float* gap, const float* W, const float* B, int O, int I,
+                                float* out) {
+  ora_sgemm_f32(W, gap, out, O, 1, I);
+  for (int o = 0; o < O; ++o) out[o] += B[o];
+}
+
+/* runtime/infer_e2e.cu:102-136 -- conv as im2col + GEMM; weights OIHW are
+ * already the GEMM A operand [OC][IC*kH*kW] (the repack loop :114-126 is an
+ * identity permutation).  One image; `col` is caller scratch of
+ * IC*kH*kW*OH*OW floats. */
+ORA_API void ora_conv2d_f32(const float* x, int IC, int H, int W, const float* w, int OC, int kH,
+                            int kW, int sH, int sW, int pH, int pW, float* col, float* y) {
+  const int OH = out_dim(H, kH, sH, pH), OW = out_dim(W, kW, sW, pW);
+  ora_im2col_nchw_f32(x, IC, H, W, kH, kW, sH, sW, pH, pW, col);
+  ora_sgemm_f32(w, col, y, OC, OH * OW, IC * kH * kW);
+}
+
+/* CUDA/MNIST_on_GPU/v3.c:125-134 + :168-174 + :161-165 -- one dense layer
+ * X[B][I] * W[I][O] (+bias, optional ReLU), plain mul-then-add order. */
+ORA_API void ora_mlp_layer_f32(const float* X, const float* Wt, const float* bias, int B, int I,
+                               int O, int relu, float* Y) {
+  for (int b = 0; b < B; ++b)
+    for (int o = 0; o < O; ++o) {
+      float acc = 0.f;
+      for (int i = 0; i < I; ++i) {
+        const float p = X[(size_t)b * I + i] * Wt[(size_t)i * O + o];
+        acc = acc + p;
+      }
+      acc = acc + bias[o];
+      if (relu) acc = fmaxf(0.f, acc);
+      Y[(size_t)b * O + o] = acc;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* int8 path (build-defined)                              */
+/* ------------------------------------------------------------------ */
+
+static inline int8_t sat_rne(float y) {
+  float q = rintf(y);
+  q = q < -127.f ? -127.f : q;
+  q = q > 127.f ? 127.f : q;
+  return (int8_t)(int)q;
+}
+
+/* Symmetric per-output-channel weight quantisation over K contiguous
+ * values: s[o] = max|w|/127 (1 if the row is all zero), q = sat(rne(w/s)). */
+ORA_API void ora_quantize_weights_s8(const float* w, int OC, int K, int8_t* q, float* scale) {
+  for (int o = 0; o < OC; ++o) {
+    float mx = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float a = fabsf(w[(size_t)o * K + k]);
+      mx = a > mx ? a : mx;
+    }
+    const float s = mx > 0.f ? mx / 127.f : 1.f;
+    scale[o] = s;
+    for (int k = 0; k < K; ++k) q[(size_t)o * K + k] = sat_rne(w[(size_t)o * K + k] / s);
+  }
+}
+
+/* Fold dequant and BN (kernels/bn_inference.cu:22-27) into one affine per
+ * output channel:  t = g/sqrtf(v+eps);  alpha = (s_x*s_w)*t;  beta = b - m*t. */
+ORA_API void ora_fold_bn(float s_x, const float* s_w, const float* g, const float* b,
+                         const float* m, const float* v, float eps, int OC, float* alpha,
+                         float* beta) {
+  for (int o = 0; o < OC; ++o) {
+    const float t = g[o] / sqrtf(v[o] + eps);
+    const float sxw = s_x * s_w[o];
+    alpha[o] = sxw * t;
+    const float mt = m[o] * t;
+    beta[o] = b[o] - mt;
+  }
+}
+
+/* fp32 -> int8 with one per-tensor scale: q = sat(rne(x * inv_s)). */
+ORA_API void ora_quantize_f32_s8(const float* x, size_t n, float inv_s, int8_t* q) {
+  for (size_t i = 0; i < n; ++i) q[i] = sat_rne(x[i] * inv_s);
+}
+
+/* im2col.cu:37-54 on int8 (one image). */
+ORA_API void ora_im2col_nchw_s8(const int8_t* x, int C, int H, int W, int kH, int kW, int sH,
+                                int sW, int pH, int pW, int8_t* col) {
+  const int OH = out_dim(H, kH, sH, pH), OW = out_dim(W, kW, sW, pW);
+  const int cs = OH * OW;
+  for (int c = 0; c < C; ++c)
+    for (int kh = 0; kh < kH; ++kh)
+      for (int kw = 0; kw < kW; ++kw) {
+        const int r = c * kH * kW + kh * kW + kw;
+        for (int oh = 0; oh < OH; ++oh)
+          for (int ow = 0; ow < OW; ++ow) {
+            const int ih = oh * sH - pH + kh, iw = ow * sW - pW + kw;
+            int8_t v = 0;
+            if (ih >= 0 && iw >= 0 && ih < H && iw < W) v = x[(size_t)c * H * W + ih * W + iw];
+            col[(size_t)r * cs + oh * OW + ow] = v;
+          }
+      }
+}
+
+/* sgemm_tiled.cu's C = A*B on int8 operands with int32 accumulation. */
+ORA_API void ora_gemm_s8s8s32(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K) {
+  for (int m = 0; m < M; ++m) {
+    int32_t* c = C + (size_t)m * N;
+    for (int n = 0; n < N; ++n) c[n] = 0;
+    for (int k = 0; k < K; ++k) {
+      const int32_t a = A[(size_t)m * K + k];
+      if (a == 0) continue;
+      const int8_t* b = B + (size_t)k * N;
+      for (int n = 0; n < N; ++n) c[n] += a * (int32_t)b[n];
+    }
+  }
+}
+
+/* conv2d_nchw_im2col_gemm (infer_e2e.cu:102-136) on int8: int32
+ * accumulators acc[N][OC][OH][OW]; w is [OC][IC*kH*kW] int8. */
+ORA_API int ora_conv2d_nchw_s8_acc(const int8_t* x, int N, int IC, int H, int W, const int8_t* w,
+                                   int OC, int kH, int kW, int sH, int sW, int pH, int pW,
+                                   int32_t* acc) {
+  const int OH = out_dim(H, kH, sH, pH), OW = out_dim(W, kW, sW, pW);
+  const size_t K = (size_t)IC * kH * kW;
+  int8_t* col = (int8_t*)malloc(K * OH * OW);
+  if (!col) return 1;
+  for (int n = 0; n < N; ++n) {
+    ora_im2col_nchw_s8(x + (size_t)n * IC * H * W, IC, H, W, kH, kW, sH, sW, pH, pW, col);
+    ora_gemm_s8s8s32(w, col, acc + (size_t)n * OC * OH * OW, OC, OH * OW, (int)K);
+  }
+  free(col);
+  return 0;
+}
+
+/* Fused epilogue (replaces bn_inference + add_inplace + relu_forward,
+ * infer_e2e.cu:168-200) on NCHW accumulators:
+ *   y = fmaf(float(acc), alpha[c], beta[c])
+ *   y = fmaf(float(res), s_r, y)          if res != NULL
+ *   y = max(y, 0)                         if relu
+ *   q = sat(rne(y * inv_s))                                            */
+ORA_API void ora_epilogue_s8(const int32_t* acc, int N, int OC, int HW, const float* alpha,
+                             const float* beta, const int8_t* res, float s_r, int relu,
+                             float inv_s, int8_t* out) {
+  for (int n = 0; n < N; ++n)
+    for (int c = 0; c < OC; ++c)
+      for (int i = 0; i < HW; ++i) {
+        const size_t idx = ((size_t)n * OC + c) * HW + i;
+        float y = fmaf((float)acc[idx], alpha[c], beta[c]);
+        if (res) y = fmaf((float)res[idx], s_r, y);
+        if (relu) y = y > 0.f ? y : 0.f;
+        out[idx] = sat_rne(y * inv_s);
+      }
+}
+
+/* fp32 epilogue (FC logits / dequant): y = fmaf(float(acc), alpha, beta). */
+ORA_API void ora_epilogue_f32(const int32_t* acc, int N, int OC, int HW, const float* alpha,
+                              const float* beta, int relu, float* out) {
+  for (int n = 0; n < N; ++n)
+    for (int c = 0; c < OC; ++c)
+      for (int i = 0; i < HW; ++i) {
+        const size_t idx = ((size_t)n * OC + c) * HW + i;
+        float y = fmaf((float)acc[idx], alpha[c], beta[c]);
+        if (relu) y = y > 0.f ? y : 0.f;
+        out[idx] = y;
+      }
+}
+
+/* maxpool2d.cu:14-40 on int8 (exact: requant is monotone). */
+ORA_API void ora_maxpool_s8(const int8_t* x, int N, int C, int H, int W, int8_t* y) {
+  const int OH = out_dim(H, 3, 2, 1), OW = out_dim(W, 3, 2, 1);
+  for (int nc = 0; nc < N * C; ++nc)
+    for (int oh = 0; oh < OH; ++oh)
+      for (int ow = 0; ow < OW; ++ow) {
+        int vmax = -128;
+        for (int kh = 0; kh < 3; ++kh) {
+          const int ih = oh * 2 - 1 + kh;
+          if (ih < 0 || ih >= H) continue;
+          for (int kw = 0; kw < 3; ++kw) {
+            const int iw = ow * 2 - 1 + kw;
+            if (iw < 0 || iw >= W) continue;
+            const int v = x[(size_t)nc * H * W + ih * W + iw];
+            vmax = v > vmax ? v : vmax;
+          }
+        }
+        y[(size_t)nc * OH * OW + oh * OW + ow] = (int8_t)vmax;
+      }
+}
+
+/* GAP (infer_e2e.cu:37-61) on int8: exact int32 channel sum, then one
+ * requant q = sat(rne(float(sum) * k)) with k = s_in/(HW*s_out) from the
+ * host.  sums (optional) receives the int32 sums [N][C]. */
+ORA_API void ora_gap_s8(const int8_t* x, int N, int C, int HW, float k, int32_t* sums,
+                        int8_t* y) {
+  for (int nc = 0; nc < N * C; ++nc) {
+    int32_t s = 0;
+    for (int i = 0; i < HW; ++i) s += x[(size_t)nc * HW + i];
+    if (sums) sums[nc] = s;
+    y[nc] = sat_rne((float)s * k);
+  }
+}
+
+/* FC (infer_e2e.cu:206-219) on int8, batched: acc[n][o] = sum_k x[n][k]*W[o][k],
+ * logits = fmaf(float(acc), alpha[o], beta[o]).  accs (optional) gets int32. */
+ORA_API void ora_fc_s8(const int8_t* x, int N, int I, const int8_t* W, int O, const float* alpha,
+                       const float* beta, int32_t* accs, float* out) {
+  for (int n = 0; n < N; ++n)
+    for (int o = 0; o < O; ++o) {
+      int32_t s = 0;
+      for (int k = 0; k < I; ++k) s += (int32_t)x[(size_t)n * I + k] * W[(size_t)o * I + k];
+      if (accs) accs[(size_t)n * O + o] = s;
+      out[(size_t)n * O + o] = fmaf((float)s, alpha[o], beta[o]);
+    }
+}
+
+/* MNIST FC layer on int8 (v4.cu:121-132 / v5.cu:131-150 semantics, W stored
+ * [in][out] as in the reference): acc[b][o] = sum_i x[b][i]*Wt[i][o]. */
+ORA_API void ora_mlp_layer_s8_acc(const int8_t* x, const int8_t* Wt, int B, int I, int O,
+                                  int32_t* acc) {
+  for (int b = 0; b < B; ++b) {
+    int32_t* c = acc + (size_t)b * O;
+    for (int o = 0; o < O; ++o) c[o] = 0;
+    for (int i = 0; i < I; ++i) {
+      const int32_t a = x[(size_t)b * I + i];
+      for (int o = 0; o < O; ++o) c[o] += a * (int32_t)Wt[(size_t)i * O + o];
+    }
+  }
+}

@@ -1,0 +1,236 @@
+"""GPU parity: every HIP kernel through the C ABI vs the CPU oracle.
+
+Bar (BASELINE.json north_star): int32 accumulators bit-exact; the fp32
+epilogue is a fixed IEEE op sequence, so int8 activations and fp32 logits
+are required bit-exact too (stricter than the 1e-6 rel the north star allows).
+The oracle works in the reference's layout (NCHW, im2col row order
+c*kH*kW+kh*kW+kw, kernels/im2col.cu:37-54); the GPU works in NHWC with K
+ordered (kh,kw,c) -- equal int32 sums prove the implicit im2col.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests.helpers import model_and_scales, nchw_to_nhwc, nhwc_to_nchw, rand_conv, rand_s8
+
+pytestmark = pytest.mark.gpu
+
+# Every conv shape of ResNet-18 (infer_e2e.cu:259-407): (name, IC, OC, k, s, p, H)
+CONV_SHAPES = [
+    ("stem", 3, 64, 7, 2, 3, 224),
+    ("l1_3x3", 64, 64, 3, 1, 1, 56),
+    ("l2_0_conv1", 64, 128, 3, 2, 1, 56),
+    ("l2_3x3", 128, 128, 3, 1, 1, 28),
+    ("l2_ds", 64, 128, 1, 2, 0, 56),
+    ("l3_0_conv1", 128, 256, 3, 2, 1, 28),
+    ("l3_3x3", 256, 256, 3, 1, 1, 14),
+    ("l3_ds", 128, 256, 1, 2, 0, 28),
+    ("l4_0_conv1", 256, 512, 3, 2, 1, 14),
+    ("l4_3x3", 512, 512, 3, 1, 1, 7),
+    ("l4_ds", 256, 512, 1, 2, 0, 14),
+]
+
+
+def _cuda(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _gpu_conv_inputs(x_nchw, wq, k):
+    from dlq_amd import ops
+    IC = wq.shape[1]
+    c_store = 4 if IC == 3 else IC
+    xh = nchw_to_nhwc(x_nchw)
+    if c_store != IC:
+        xh = np.concatenate([xh, np.zeros(xh.shape[:3] + (c_store - IC,), np.int8)], axis=3)
+    packed = ops.pack_conv_weights(wq, c_store)
+    return _cuda(xh), _cuda(packed)
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES, ids=[s[0] for s in CONV_SHAPES])
+def test_conv_int32_accumulators_bitexact(gpu, shape):
+    from dlq_amd import ops
+    from dlq_amd.lib import DLQ_OUT_S32
+    name, IC, OC, k, s, p, H = shape
+    rng = np.random.default_rng(sum(map(ord, name)) * 7919)
+    N = 2 if H >= 56 else 3  # ragged: 3*OH*OW is not a multiple of the pixel tile
+    x = rand_s8(rng, (N, IC, H, H))
+    w, _ = rand_conv(rng, OC, IC, k)
+    wq, _ = O.quantize_weights_s8(w)
+    ref = O.conv_s8_acc(x, wq, s, p)
+    xd, wd = _gpu_conv_inputs(x, wq, k)
+    acc = ops.conv2d_nhwc_s8(xd, wd, OC, k, s, p, out_kind=DLQ_OUT_S32)
+    got = nhwc_to_nchw(acc.cpu().numpy())
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref), f"{name}: {np.count_nonzero(got != ref)} int32 mismatches"
+
+
+@pytest.mark.parametrize("shape", [CONV_SHAPES[i] for i in (0, 1, 2, 4, 6, 9)],
+                         ids=[CONV_SHAPES[i][0] for i in (0, 1, 2, 4, 6, 9)])
+@pytest.mark.parametrize("residual", [False, True])
+def test_conv_fused_epilogue_bitexact(gpu, shape, residual):
+    from dlq_amd import ops
+    name, IC, OC, k, s, p, H = shape
+    if residual and IC == 3:
+        pytest.skip("the stem has no residual input")
+    rng = np.random.default_rng(7 + sum(map(ord, name)))
+    N = 2
+    x = rand_s8(rng, (N, IC, H, H))
+    w, bn = rand_conv(rng, OC, IC, k)
+    wq, sw = O.quantize_weights_s8(w)
+    s_x, s_y, s_r = 0.031, 0.047, 0.052
+    alpha, beta = O.fold_bn(s_x, sw, bn)
+    acc = O.conv_s8_acc(x, wq, s, p)
+    res = rand_s8(rng, acc.shape) if residual else None
+    relu = (k != 1)  # downsample convs have no ReLU (infer_e2e.cu:187-196)
+    ref = O.epilogue_s8(acc, alpha, beta, s_y, res, s_r, relu)
+    xd, wd = _gpu_conv_inputs(x, wq, k)
+    ocp = ops.packed_oc(OC)
+    a_alpha, a_beta = ops.fold_bn(s_x, sw, *bn)
+    assert np.array_equal(a_alpha, alpha) and np.array_equal(a_beta, beta)  # host prep == oracle
+    y = ops.conv2d_nhwc_s8(xd, wd, OC, k, s, p, _cuda(ops.pad_vec(a_alpha, ocp)), _cuda(ops.pad_vec(a_beta, ocp)),
+                           residual=_cuda(nchw_to_nhwc(res)) if residual else None, res_scale=s_r,
+                           out_scale=s_y, relu=relu)
+    got = nhwc_to_nchw(y.cpu().numpy())
+    assert np.array_equal(got, ref), f"{name}: {np.count_nonzero(got != ref)} int8 mismatches"
+
+
+def test_fc_logits_bitexact(gpu):
+    from dlq_amd import ops
+    from dlq_amd.lib import DLQ_OUT_F32, DLQ_OUT_S32
+    from tests.helpers import golden
+    rng = np.random.default_rng(11)
+    W = golden("fc.weight.bin", (1000, 512))  # the reference's real FC weights (tmp_e2e/)
+    bias = golden("fc.bias.bin")
+    wq, sw = O.quantize_weights_s8(W)
+    for N in (1, 7, 256):
+        x = rand_s8(rng, (N, 512), lo=0)
+        alpha = O.fc_alpha(0.02, sw)
+        ref, racc = O.fc_s8(x, wq, alpha, bias)
+        packed = _cuda(ops.pack_conv_weights(wq.reshape(1000, 512, 1, 1), 512))
+        ocp = ops.packed_oc(1000)
+        acc = ops.linear_s8(_cuda(x), packed, 1000, out_kind=DLQ_OUT_S32)
+        assert np.array_equal(acc.cpu().numpy(), racc)
+        out = ops.linear_s8(_cuda(x), packed, 1000, _cuda(ops.pad_vec(alpha, ocp)), _cuda(ops.pad_vec(bias, ocp)),
+                            out_kind=DLQ_OUT_F32)
+        assert np.array_equal(out.cpu().numpy().view(np.int32), ref.view(np.int32))
+
+
+def test_quantize_input_bitexact(gpu):
+    from dlq_amd import ops
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal((3, 3, 224, 224), dtype=np.float32) * 1.3).astype(np.float32)
+    x[0, 0, 0, :8] = [0.5, 1.5, 2.5, -0.5, -1.5, 1e9, -1e9, 0.0]  # ties and saturation
+    s = 2.64 / 127
+    ref = O.quantize_f32_s8(x, s)
+    y = ops.quantize_nchw_to_nhwc(_cuda(x), s, 4).cpu().numpy()
+    assert np.all(y[..., 3] == 0)
+    assert np.array_equal(nhwc_to_nchw(y[..., :3]), ref)
+
+
+def test_maxpool_and_gap_bitexact(gpu):
+    from dlq_amd import ops
+    rng = np.random.default_rng(5)
+    x = rand_s8(rng, (3, 64, 112, 112), lo=-128)
+    ref = O.maxpool_s8(x)
+    got = nhwc_to_nchw(ops.maxpool2d_3x3_s2p1_nhwc_s8(_cuda(nchw_to_nhwc(x))).cpu().numpy())
+    assert np.array_equal(got, ref)
+    x4 = rand_s8(rng, (5, 512, 7, 7))
+    k = O.gap_k(0.05, 49, 0.011)
+    gref, _ = O.gap_s8(x4, k)
+    ggot = ops.gap_nhwc_s8(_cuda(nchw_to_nhwc(x4)), float(k)).cpu().numpy()
+    assert np.array_equal(ggot, gref)
+
+
+def test_im2col_reference_order_bitexact(gpu):
+    from dlq_amd import ops
+    rng = np.random.default_rng(9)
+    for (C, H, k, s, p) in [(3, 224, 7, 2, 3), (64, 56, 3, 1, 1), (128, 28, 1, 2, 0)]:
+        x = rand_s8(rng, (2, C, H, H))
+        col = ops.im2col_nchw_s8(_cuda(x), k, s, p).cpu().numpy()
+        for n in range(2):
+            OH = O.out_dim(H, k, s, p)
+            ref = np.empty(C * k * k * OH * OH, np.int8)
+            O.lib().ora_im2col_nchw_s8(x[n].copy(), C, H, H, k, k, s, s, p, p, ref)
+            assert np.array_equal(col[n].reshape(-1), ref)
+
+
+def _stage_nchw(model, name, B):
+    shapes = {"stem_pool": (56, 56, 64), "layer1": (56, 56, 64), "layer2": (28, 28, 128),
+              "layer3": (14, 14, 256), "layer4": (7, 7, 512), "conv1": (112, 112, 64)}
+    if name == "gap":
+        return model.stage("gap", (B, 512)).cpu().numpy()
+    h, w, c = shapes[name]
+    return nhwc_to_nchw(model.stage(name, (B, h, w, c)).cpu().numpy())
+
+
+def test_resnet18_end_to_end_bitexact(gpu):
+    """Whole network, B=2: every stage's int8 activations and the fp32 logits."""
+    from dlq_amd.models import ResNet18Int8, synthetic_images
+    sd, scales = model_and_scales()
+    x = synthetic_images(2, seed=77).numpy()
+    ref_logits, dumps = O.resnet18_forward_s8(sd, scales, x)
+    model = ResNet18Int8(sd, scales, max_batch=4, keep_stages=True)
+    logits = model(_cuda(x)).cpu().numpy()
+    torch.cuda.synchronize()
+    for st in ("conv1", "stem_pool", "layer1", "layer2", "layer3", "layer4", "gap"):
+        got = _stage_nchw(model, st, 2)
+        assert np.array_equal(got, dumps[st]), f"stage {st}: {np.count_nonzero(got != dumps[st])} mismatches"
+    assert np.array_equal(logits.view(np.int32), ref_logits.view(np.int32))
+
+
+def test_resnet18_batch_invariance_full_batch(gpu):
+    """Batch 256 (the benchmark config): each image's logits are bit-identical
+    to the same image run alone, and to the oracle on a sample."""
+    from dlq_amd.models import ResNet18Int8, synthetic_images
+    sd, scales = model_and_scales()
+    x = synthetic_images(256, seed=99).cuda()
+    model = ResNet18Int8(sd, scales, max_batch=256)
+    big = model(x).cpu().numpy()
+    again = model(x).cpu().numpy()
+    assert np.array_equal(big.view(np.int32), again.view(np.int32))  # deterministic
+    for i in (0, 1, 128, 255):
+        one = model(x[i:i + 1].contiguous()).cpu().numpy()
+        assert np.array_equal(one[0].view(np.int32), big[i].view(np.int32))
+    ref, _ = O.resnet18_forward_s8(sd, scales, x[[0, 255]].cpu().numpy())
+    assert np.array_equal(ref.view(np.int32), big[[0, 255]].view(np.int32))
+
+
+def test_resnet18_empty_and_oversize_batch(gpu):
+    from dlq_amd.lib import DLQError
+    from dlq_amd.models import ResNet18Int8
+    sd, scales = model_and_scales()
+    model = ResNet18Int8(sd, scales, max_batch=2)
+    out = model(torch.empty((0, 3, 224, 224), device="cuda"))
+    assert out.shape == (0, 1000)
+    with pytest.raises(DLQError):
+        model(torch.zeros((3, 3, 224, 224), device="cuda"))
+
+
+@pytest.mark.parametrize("hidden", [256, 128])
+def test_mnist_mlp_bitexact(gpu, hidden):
+    """MNIST FC path (v4.cu:255-302 / v5.cu:127-157) at batch 1024, int8."""
+    from dlq_amd.models import MLPInt8, mlp_weights
+    from dlq_amd.quant import calibrate_mlp
+    W1, b1, W2, b2 = mlp_weights(784, hidden, 10)
+    rng = np.random.default_rng(21)
+    x = ((rng.random((1024, 784), dtype=np.float32) - np.float32(0.1307)) / np.float32(0.3081)).astype(np.float32)
+    s_in, s_h = calibrate_mlp(W1, b1, x)
+    # oracle: quantise, int32 GEMM in the reference [in][out] layout, epilogues
+    xq = O.quantize_f32_s8(x, s_in)
+    q1, sw1 = O.quantize_weights_s8(W1.T.copy())
+    q2, sw2 = O.quantize_weights_s8(W2.T.copy())
+    acc1 = np.empty((1024, hidden), np.int32)
+    O.lib().ora_mlp_layer_s8_acc(xq, q1.T.copy(), 1024, 784, hidden, acc1)
+    h = O.epilogue_s8(acc1[:, :, None], O.fc_alpha(s_in, sw1), b1, s_h, relu=True)[:, :, 0]
+    acc2 = np.empty((1024, 10), np.int32)
+    O.lib().ora_mlp_layer_s8_acc(h, q2.T.copy(), 1024, hidden, 10, acc2)
+    ref = np.empty((1024, 10), np.float32)
+    O.lib().ora_epilogue_f32(acc2.reshape(-1), 1024, 10, 1, O.fc_alpha(s_h, sw2), b2, 0, ref)
+    m = MLPInt8(W1, b1, W2, b2, s_in, s_h, max_batch=1024)
+    out = m(_cuda(x)).cpu().numpy()
+    assert np.array_equal(m.hidden_q(1024).cpu().numpy(), h)
+    assert np.array_equal(out.view(np.int32), ref.view(np.int32))
+    for B in (1, 3, 77):
+        o2 = m(_cuda(x[:B])).cpu().numpy()
+        assert np.array_equal(o2.view(np.int32), ref[:B].view(np.int32))
