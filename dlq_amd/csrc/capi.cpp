@@ -3,6 +3,7 @@
 // operator entry points.  Errors are returned, never exit()ed (the reference's
 // CUDA_CHECK exits: CUDA/resnet18-kernel-lab/cpp/fp32/runtime/utils.hpp:23-32).
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -13,6 +14,14 @@
 namespace dlq {
 
 static thread_local std::string g_err;
+
+int debug_bits() {
+  static const int bits = [] {
+    const char* e = std::getenv("DLQ_DBG");
+    return e ? std::atoi(e) : 0;
+  }();
+  return bits;
+}
 
 void set_error(const std::string& msg) { g_err = msg; }
 int fail(int code, const std::string& msg) {
@@ -63,18 +72,31 @@ size_t packed_bytes(int OC, int C, int kH, int kW) {
   return ocp * (size_t)kH * kW * C;
 }
 
+size_t packed_offset(int oc, int tap, int c, int OCp, int taps) {
+  const int ch = c >> 6, lc = (c >> 4) & 3, b = c & 15, ot = oc >> 6, ol = oc & 63;
+  const int pch = lc ^ ((ol >> 2) & 3);
+  return (((size_t)ch * (OCp / 64) + ot) * 64 + ol) * ((size_t)taps * 64) + (size_t)tap * 64 +
+         pch * 16 + b;
+}
+
 void pack_conv_weights(const int8_t* q, int OC, int IC, int kH, int kW, int C, int8_t* out) {
   const size_t total = packed_bytes(OC, C, kH, kW);
   std::memset(out, 0, total);
-  const bool stem = is_stem(C, kH, kW);
-  const int kw_p = stem ? 8 : kW;                 // padded taps per row
-  const size_t K = stem ? (size_t)kStemK : (size_t)kH * kW * C;
+  if (is_stem(C, kH, kW)) {  // [OCp][8][8][4]: 7x7 taps padded to 8x8, RGB + zero channel
+    for (int o = 0; o < OC; ++o)
+      for (int c = 0; c < IC; ++c)
+        for (int kh = 0; kh < kH; ++kh)
+          for (int kw = 0; kw < kW; ++kw)
+            out[(size_t)o * kStemK + ((size_t)kh * 8 + kw) * C + c] =
+                q[(((size_t)o * IC + c) * kH + kh) * kW + kw];
+    return;
+  }
+  const int OCp = packed_oc(OC), taps = kH * kW;
   for (int o = 0; o < OC; ++o)
     for (int c = 0; c < IC; ++c)
       for (int kh = 0; kh < kH; ++kh)
         for (int kw = 0; kw < kW; ++kw)
-          out[(size_t)o * K + ((size_t)kh * kw_p + kw) * C + c] =
-              q[(((size_t)o * IC + c) * kH + kh) * kW + kw];
+          out[packed_offset(o, kh * kW + kw, c, OCp, taps)] = q[(((size_t)o * IC + c) * kH + kh) * kW + kw];
 }
 
 }  // namespace dlq
@@ -159,6 +181,7 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
   a.K = is_stem(d->C, d->kH, d->kW) ? kStemK : d->kH * d->kW * d->C;
   a.kH = d->kH; a.kW = d->kW; a.sH = d->sH; a.sW = d->sW; a.pH = d->pH; a.pW = d->pW;
   a.relu = relu ? 1 : 0; a.out_kind = out_kind;
+  a.dbg = debug_bits();
   if (a.OH <= 0 || a.OW <= 0) return fail(DLQ_ERR_ARG, "conv2d: empty output");
   const long long P = (long long)a.N * a.OH * a.OW;
   const long long in_bytes = (long long)a.N * a.H * a.W * a.C;

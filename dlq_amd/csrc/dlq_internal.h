@@ -24,7 +24,11 @@ struct ConvArgs {
   int P;     // N*OH*OW
   int relu;
   int out_kind;
+  int dbg;  // ablation bits for timing builds (0 in every real call): 1 skip MFMA, 2 skip DMA, 4 skip stores
 };
+
+// Ablation bits from the DLQ_DBG environment variable (read once; 0 = off).
+int debug_bits();
 
 // Stem packing: C == 4, 7x7 taps padded to 8x8 -> K = 256.
 constexpr int kStemC = 4;
@@ -33,8 +37,10 @@ constexpr int kStemK = 8 * 8 * 4;
 int packed_oc(int OC);
 bool is_stem(int C, int kH, int kW);
 
-// Kernel launchers (kernels.hip).  Return hipError_t of the launch.
+// Kernel launchers (kernels.hip, conv3x3.hip).  Return hipError_t of the launch.
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s);
+bool conv3x3s1_supported(const ConvArgs& a);
+hipError_t launch_conv3x3s1(const ConvArgs& a, hipStream_t s);
 hipError_t launch_quantize_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cout,
                                         float inv_s, int8_t* y, hipStream_t s);
 hipError_t launch_quantize_rows(const float* x, int rows, int cols, int ldy, float inv_s,

@@ -23,37 +23,12 @@
 //   A: lane l holds W[row l&31][k 16*(l>>5) .. +15]
 //   B: lane l holds X[col l&31][k 16*(l>>5) .. +15]
 //   D: reg r of lane l is D[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31]
-#include "dlq_internal.h"
+#include <cstdlib>
+
+#include "device_common.h"
 
 namespace dlq {
 namespace {
-
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v16i __attribute__((ext_vector_type(16)));
-typedef signed char v16c __attribute__((ext_vector_type(16)));
-
-constexpr int BK = 64;   // K bytes per pipeline step = two 32-deep MFMA k-steps
-constexpr int NT = 256;  // threads per conv workgroup (4 waves)
-
-// 16-byte chunk swizzle inside a 64-byte LDS row: lanes of one ds_read_b128
-// group read 16 different rows at the same chunk; XOR with (row>>2)&3 spreads
-// them over all 64 banks (MI355X_MICROARCH.md §LDS lane groups).
-__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
-
-__device__ __forceinline__ int sat_rne(float y) {
-  float q = __builtin_rintf(y);
-  q = q < -127.f ? -127.f : q;
-  q = q > 127.f ? 127.f : q;
-  return (int)q;
-}
-
-// Bijective XCD-aware remap: consecutive logical tiles land on one XCD
-// (cdna_hip_programming.md §5 "XCD swizzle must be bijective").
-__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
-  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  return base + (bid >> 3);
-}
 
 template <int TOC, int TP, int WOC>
 struct TileCfg {
@@ -106,16 +81,21 @@ __global__ __launch_bounds__(NT) void conv_s8_kernel(ConvArgs a) {
       pbase[i] = 0;
     }
   }
-  const int8_t* wrow = a.w + (size_t)(oc0 + srow) * K + sch * 16;
+  // Weight rows: MODE 0 reads the chunk-major packed image (capi.cpp
+  // packed_offset); this thread's rows are oc0 + srow + 64*i, so oc%64 == srow.
+  const int taps = a.kH * a.kW, n_ot = a.OCp / 64;
+  const int wsw = (sch ^ ((srow >> 2) & 3)) * 16;
+  const int8_t* wrow = a.w + (size_t)(oc0 + srow) * K + sch * 16;  // MODE 1 (stem) layout
 
   v4i ra[T::ALD], rb[T::BLD];
   auto gload = [&](int ks) {
-#pragma unroll
-    for (int i = 0; i < T::ALD; ++i)
-      ra[i] = *(const v4i*)(wrow + (size_t)(64 * i) * K + ks * BK);
     if constexpr (MODE == 0) {
       const int cpt = C / BK;  // K steps per tap
-      const int tap = ks / cpt, cb = (ks - tap * cpt) * BK;
+      const int tap = ks / cpt, ch = ks - tap * cpt, cb = ch * BK;
+#pragma unroll
+      for (int i = 0; i < T::ALD; ++i)
+        ra[i] = *(const v4i*)(a.w + (((size_t)ch * n_ot + oc0 / 64 + i) * 64 + srow) * (taps * 64) +
+                              tap * 64 + wsw);
       const int kh = tap / a.kW, kw = tap - kh * a.kW;
 #pragma unroll
       for (int i = 0; i < T::BLD; ++i) {
@@ -126,6 +106,8 @@ __global__ __launch_bounds__(NT) void conv_s8_kernel(ConvArgs a) {
           rb[i] = v4i{0, 0, 0, 0};
       }
     } else {
+#pragma unroll
+      for (int i = 0; i < T::ALD; ++i) ra[i] = *(const v4i*)(wrow + (size_t)(64 * i) * K + ks * BK);
       const int kh = 2 * ks + (sch >> 1), kw0 = (sch & 1) * 4;
 #pragma unroll
       for (int i = 0; i < T::BLD; ++i) {
@@ -433,6 +415,11 @@ int packed_oc(int OC) { return OC <= 64 ? 64 : (OC + 127) / 128 * 128; }
 bool is_stem(int C, int kH, int kW) { return C == kStemC && kH == 7 && kW == 7; }
 
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
+  static const bool force_v1 = [] {
+    const char* e = std::getenv("DLQ_CONV_V1");
+    return e && e[0] == '1';
+  }();
+  if (!force_v1 && conv3x3s1_supported(a)) return launch_conv3x3s1(a, s);
   if (is_stem(a.C, a.kH, a.kW)) return launch_cfg<64, 256, 1, 1>(a, s);
   if (a.OCp == 64) return launch_cfg<64, 256, 1, 0>(a, s);
   return launch_cfg<128, 128, 2, 0>(a, s);

@@ -74,7 +74,13 @@ int dlq_conv_packed_oc(int OC);
  * kH == kW == 7).  Returns 0 for unsupported shapes. */
 size_t dlq_conv_packed_bytes(int OC, int C, int kH, int kW);
 /* Pack int8 OIHW weights q[OC][IC][kH][kW] (IC <= C; channels IC..C-1 and
- * padded rows are zero) into the kernel's [OCp][K] image. */
+ * padded rows are zero) into the kernels' image.  C % 64 == 0:
+ *   [C/64][OCp/64][64 oc][kH*kW taps][4 x 16-byte chunks][16]
+ * i.e. per (64-channel chunk, 64-output-channel tile) one contiguous block
+ * that is copied verbatim into LDS; the 4 chunks of a 64-byte tap row are
+ * stored at position chunk ^ ((oc%64 >> 2) & 3) (bank-conflict-free
+ * ds_read_b128 of 16 consecutive output channels).
+ * Stem (C == 4, 7x7): [OCp][8][8][4], taps padded to 8x8. */
 int dlq_pack_conv_weights_s8(const int8_t* q_oihw, int OC, int IC, int kH, int kW, int C,
                              int8_t* packed);
 

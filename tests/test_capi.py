@@ -58,10 +58,19 @@ def test_pack_layout():
     pads 7x7 taps to 8x8 and 3 channels to 4."""
     from dlq_amd import ops
     rng = np.random.default_rng(1)
-    q = rng.integers(-127, 128, size=(100, 64, 3, 3), dtype=np.int8)
-    p = ops.pack_conv_weights(q, 64).reshape(ops.packed_oc(100), 3, 3, 64)
-    assert np.array_equal(p[:100], np.transpose(q, (0, 2, 3, 1)))
-    assert not p[100:].any()
+    q = rng.integers(-127, 128, size=(100, 128, 3, 3), dtype=np.int8)
+    ocp = ops.packed_oc(100)
+    # [C/64][OCp/64][64 oc][9 taps][4 chunks of 16, stored at chunk ^ ((oc%64>>2)&3)]
+    p = ops.pack_conv_weights(q, 128).reshape(2, ocp // 64, 64, 9, 4, 16)
+    oc = np.arange(ocp).reshape(ocp // 64, 64)
+    perm = (np.arange(4)[None, :] ^ ((np.arange(64)[:, None] >> 2) & 3))  # [ol][logical chunk] -> stored pos
+    logical = np.empty_like(p)
+    for ol in range(64):
+        for lc in range(4):
+            logical[:, :, ol, :, lc, :] = p[:, :, ol, :, perm[ol, lc], :]
+    dense = logical.transpose(1, 2, 3, 0, 4, 5).reshape(ocp, 3, 3, 128)  # [OCp][kh][kw][c]
+    assert np.array_equal(dense[:100], np.transpose(q, (0, 2, 3, 1)))
+    assert not dense[100:].any() and oc.size == ocp
     qs = rng.integers(-127, 128, size=(64, 3, 7, 7), dtype=np.int8)
     ps = ops.pack_conv_weights(qs, 4).reshape(64, 8, 8, 4)
     assert np.array_equal(ps[:, :7, :7, :3], np.transpose(qs, (0, 2, 3, 1)))
