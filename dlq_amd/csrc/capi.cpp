@@ -54,15 +54,20 @@ void quantize_weights(const float* w, int OC, int K, int8_t* q, float* scale) {
 }
 
 void fold_bn(float s_x, const float* s_w, const float* g, const float* b, const float* m,
-             const float* v, float eps, int OC, float* alpha, float* beta) {
+             const float* v, float eps, float s_y, int OC, float* alpha, float* beta) {
+  const float inv_y = 1.0f / s_y;
   for (int o = 0; o < OC; ++o) {
     const float t = g[o] / std::sqrt(v[o] + eps);
     const float sxw = s_x * s_w[o];
-    alpha[o] = sxw * t;
+    const float a = sxw * t;
+    alpha[o] = a * inv_y;
     const float mt = m[o] * t;
-    beta[o] = b[o] - mt;
+    const float bb = b[o] - mt;
+    beta[o] = bb * inv_y;
   }
 }
+
+float res_scale(float s_r, float s_y) { return s_r * (1.0f / s_y); }
 
 size_t packed_bytes(int OC, int C, int kH, int kW) {
   if (OC <= 0 || C <= 0) return 0;
@@ -123,12 +128,14 @@ int dlq_quantize_weights_s8(const float* w, int OC, int K, int8_t* q, float* sca
 }
 
 int dlq_fold_bn(float s_x, const float* s_w, const float* g, const float* b, const float* m,
-                const float* v, float eps, int OC, float* alpha, float* beta) {
-  if (!s_w || !g || !b || !m || !v || !alpha || !beta || OC <= 0)
+                const float* v, float eps, float s_y, int OC, float* alpha, float* beta) {
+  if (!s_w || !g || !b || !m || !v || !alpha || !beta || OC <= 0 || !(s_y > 0.f))
     return fail(DLQ_ERR_ARG, "fold_bn: bad args");
-  fold_bn(s_x, s_w, g, b, m, v, eps, OC, alpha, beta);
+  fold_bn(s_x, s_w, g, b, m, v, eps, s_y, OC, alpha, beta);
   return DLQ_OK;
 }
+
+float dlq_res_scale(float s_r, float s_y) { return res_scale(s_r, s_y); }
 
 int dlq_conv_packed_oc(int OC) { return OC > 0 ? packed_oc(OC) : 0; }
 
@@ -161,8 +168,7 @@ int dlq_quantize_rows_s8(const float* x, int rows, int cols, int ldy, float inv_
 
 int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
                        const float* alpha, const float* beta, const int8_t* residual,
-                       float res_scale, float inv_out_scale, int relu, int out_kind, void* y,
-                       void* stream) {
+                       float res_scale, int relu, int out_kind, void* y, void* stream) {
   if (!d || !x || !w_packed || !y) return fail(DLQ_ERR_ARG, "conv2d: null pointer");
   if (out_kind < 0 || out_kind > 2) return fail(DLQ_ERR_ARG, "conv2d: bad out_kind");
   if (out_kind != DLQ_OUT_S32 && (!alpha || !beta)) return fail(DLQ_ERR_ARG, "conv2d: alpha/beta required");
@@ -173,7 +179,7 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
     return fail(DLQ_ERR_ARG, "conv2d: unsupported C (need C%64==0, or C==4 with a 7x7 kernel)");
   ConvArgs a{};
   a.x = x; a.w = w_packed; a.alpha = alpha; a.beta = beta; a.res = residual; a.y = y;
-  a.s_res = res_scale; a.inv_s = inv_out_scale;
+  a.s_res = res_scale;
   a.N = d->N; a.H = d->H; a.W = d->W; a.C = d->C;
   a.OH = out_dim(d->H, d->kH, d->sH, d->pH);
   a.OW = out_dim(d->W, d->kW, d->sW, d->pW);
@@ -199,12 +205,10 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
 }
 
 int dlq_linear_s8(const int8_t* x, int N, int K, const int8_t* w_packed, int OC, const float* alpha,
-                  const float* beta, float inv_out_scale, int relu, int out_kind, void* y,
-                  void* stream) {
+                  const float* beta, int relu, int out_kind, void* y, void* stream) {
   if (K <= 0 || K % 64) return fail(DLQ_ERR_ARG, "linear: K must be a positive multiple of 64");
   dlq_conv_desc d{N, 1, 1, K, OC, 1, 1, 1, 1, 0, 0};
-  return dlq_conv2d_nhwc_s8(&d, x, w_packed, alpha, beta, nullptr, 0.f, inv_out_scale, relu,
-                            out_kind, y, stream);
+  return dlq_conv2d_nhwc_s8(&d, x, w_packed, alpha, beta, nullptr, 0.f, relu, out_kind, y, stream);
 }
 
 int dlq_maxpool2d_3x3_s2p1_nhwc_s8(const int8_t* x, int N, int C, int H, int W, int8_t* y,

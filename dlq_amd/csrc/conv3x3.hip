@@ -306,14 +306,13 @@ __global__ __launch_bounds__(NWAVE * 64, 1) void conv3x3s1_kernel(ConvArgs a) {
               const float alv[4] = {al.x, al.y, al.z, al.w};
               const float bev[4] = {be.x, be.y, be.z, be.w};
               const int rq = e_rq[fm][fn][g];
-              unsigned packed = 0;
+              float v[4];
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
-                float v = __builtin_fmaf((float)acc[fm][fn][4 * g + j], alv[j], bev[j]);
-                if constexpr (RES) v = __builtin_fmaf((float)(int)(signed char)(rq >> (8 * j)), a.s_res, v);
-                if (a.relu) v = v > 0.f ? v : 0.f;
-                packed |= ((unsigned)sat_rne(v * a.inv_s) & 0xffu) << (8 * j);
+                v[j] = __builtin_fmaf((float)acc[fm][fn][4 * g + j], alv[j], bev[j]);
+                if constexpr (RES) v[j] = __builtin_fmaf((float)(int)(signed char)(rq >> (8 * j)), a.s_res, v[j]);
               }
+              const unsigned packed = quant4(v[0], v[1], v[2], v[3], a.relu ? 0.f : -127.f);
               *(unsigned*)(sb + pl * 64 + (((ol >> 4) ^ ((pl >> 2) & 3)) << 4) + ((ol >> 2) & 3) * 4) = packed;
             }
         }

@@ -24,6 +24,21 @@ __device__ __forceinline__ int sat_rne(float y) {
   return (int)q;
 }
 
+// Fused-epilogue requantisation of 4 values already in output-grid units:
+// q = rne(clamp(y, lo, 127)) packed as 4 x int8.  clamp = one v_med3_f32;
+// adding 1.5*2^23 rounds to nearest-even and leaves q in the low mantissa
+// bits (two's complement in the low byte for |q| <= 127); two v_perm_b32 + or
+// pack the bytes.  Bit-identical to oracle.c ora_epilogue_s8's
+// rintf(clamp(y)).
+__device__ __forceinline__ unsigned quant4(float y0, float y1, float y2, float y3, float lo) {
+  const float M = 12582912.0f;
+  const unsigned u0 = __float_as_uint(__builtin_amdgcn_fmed3f(y0, lo, 127.f) + M);
+  const unsigned u1 = __float_as_uint(__builtin_amdgcn_fmed3f(y1, lo, 127.f) + M);
+  const unsigned u2 = __float_as_uint(__builtin_amdgcn_fmed3f(y2, lo, 127.f) + M);
+  const unsigned u3 = __float_as_uint(__builtin_amdgcn_fmed3f(y3, lo, 127.f) + M);
+  return __builtin_amdgcn_perm(u1, u0, 0x0c0c0400u) | __builtin_amdgcn_perm(u3, u2, 0x04000c0cu);
+}
+
 // Bijective XCD-aware remap: consecutive logical tiles land on one XCD
 // (cdna_hip_programming.md §5 "XCD swizzle must be bijective").
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

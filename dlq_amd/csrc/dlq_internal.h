@@ -16,8 +16,7 @@ struct ConvArgs {
   const float* beta;    // [OCp]
   const int8_t* res;    // [N][OH][OW][OC] or nullptr
   void* y;              // [N][OH][OW][OC] (int8 / fp32 / int32)
-  float s_res;
-  float inv_s;
+  float s_res;  // residual scale in output-grid units
   int N, H, W, C;
   int OH, OW, OC, OCp, K;
   int kH, kW, sH, sW, pH, pW;
@@ -58,7 +57,8 @@ int hip_fail(hipError_t e, const char* what);
 // Host weight preparation (capi.cpp), identical op order to oracle/oracle.c.
 void quantize_weights(const float* w, int OC, int K, int8_t* q, float* scale);
 void fold_bn(float s_x, const float* s_w, const float* g, const float* b, const float* m,
-             const float* v, float eps, int OC, float* alpha, float* beta);
+             const float* v, float eps, float s_y, int OC, float* alpha, float* beta);
+float res_scale(float s_r, float s_y);
 size_t packed_bytes(int OC, int C, int kH, int kW);
 void pack_conv_weights(const int8_t* q_oihw, int OC, int IC, int kH, int kW, int C,
                        int8_t* packed);

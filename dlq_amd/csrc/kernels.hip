@@ -221,15 +221,10 @@ __global__ __launch_bounds__(NT) void conv_s8_kernel(ConvArgs a) {
           } else {
             int rq = 0;
             if constexpr (RES) rq = *(const int*)(a.res + o);
-            unsigned packed = 0;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              float v = y[j];
-              if constexpr (RES) v = __builtin_fmaf((float)(int)(signed char)(rq >> (8 * j)), a.s_res, v);
-              if (a.relu) v = v > 0.f ? v : 0.f;
-              packed |= ((unsigned)sat_rne(v * a.inv_s) & 0xffu) << (8 * j);
-            }
-            *(unsigned*)((int8_t*)a.y + o) = packed;
+            for (int j = 0; j < 4; ++j)
+              if constexpr (RES) y[j] = __builtin_fmaf((float)(int)(signed char)(rq >> (8 * j)), a.s_res, y[j]);
+            *(unsigned*)((int8_t*)a.y + o) = quant4(y[0], y[1], y[2], y[3], a.relu ? 0.f : -127.f);
           }
         }
       }

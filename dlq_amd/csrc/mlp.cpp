@@ -41,9 +41,11 @@ int up(dlq_mlp* m, void** dst, const void* src, size_t bytes) {
 }
 
 // Reference layout W[in][out] (v4.cu:121-132) -> per-output-channel int8
-// rows, packed [OCp][kp]; alpha = s_x * s_w[o], beta = bias[o].
+// rows, packed [OCp][kp]; alpha = s_x * s_w[o], beta = bias[o] -- for an int8
+// output (s_y > 0) both in output-grid units: alpha = (s_x*s_w[o])*(1/s_y),
+// beta = bias[o]*(1/s_y) (the convention of dlq_fold_bn).
 int prep_layer(dlq_mlp* m, const float* Wt, const float* bias, int in, int out, int kp, float s_x,
-               int8_t** dw, float** da, float** db) {
+               float s_y, int8_t** dw, float** da, float** db) {
   std::vector<float> w((size_t)out * in);
   for (int i = 0; i < in; ++i)
     for (int o = 0; o < out; ++o) w[(size_t)o * in + i] = Wt[(size_t)i * out + o];
@@ -54,9 +56,11 @@ int prep_layer(dlq_mlp* m, const float* Wt, const float* bias, int in, int out, 
   pack_conv_weights(q.data(), out, in, 1, 1, kp, packed.data());
   const int op = packed_oc(out);
   std::vector<float> a(op, 0.f), b(op, 0.f);
+  const float inv_y = s_y > 0.f ? 1.0f / s_y : 1.0f;
   for (int o = 0; o < out; ++o) {
-    a[o] = s_x * sw[o];
-    b[o] = bias[o];
+    const float sa = s_x * sw[o];
+    a[o] = s_y > 0.f ? sa * inv_y : sa;
+    b[o] = s_y > 0.f ? bias[o] * inv_y : bias[o];
   }
   int rc;
   if ((rc = up(m, (void**)dw, packed.data(), packed.size())) || (rc = up(m, (void**)da, a.data(), op * 4)) ||
@@ -81,8 +85,8 @@ int dlq_mlp_create(int in, int hidden, int out, const float* W1, const float* b1
   m->in = in; m->hidden = hidden; m->out = out; m->kp = (in + 63) / 64 * 64;
   m->max_batch = max_batch; m->s_in = s_in; m->s_hidden = s_hidden;
   int rc;
-  if ((rc = prep_layer(m, W1, b1, in, hidden, m->kp, s_in, &m->w1, &m->a1, &m->b1)) ||
-      (rc = prep_layer(m, W2, b2, hidden, out, hidden, s_hidden, &m->w2, &m->a2, &m->b2)) ||
+  if ((rc = prep_layer(m, W1, b1, in, hidden, m->kp, s_in, s_hidden, &m->w1, &m->a1, &m->b1)) ||
+      (rc = prep_layer(m, W2, b2, hidden, out, hidden, s_hidden, 0.f, &m->w2, &m->a2, &m->b2)) ||
       (rc = up(m, (void**)&m->xq, nullptr, (size_t)max_batch * m->kp)) ||
       (rc = up(m, (void**)&m->hq, nullptr, (size_t)max_batch * hidden))) {
     dlq_mlp_destroy(m);
@@ -105,11 +109,9 @@ int dlq_mlp_forward(dlq_mlp* m, const float* x, int B, float* logits, void* stre
   if (!x || !logits) return fail(DLQ_ERR_ARG, "mlp_forward: null argument");
   int rc = dlq_quantize_rows_s8(x, B, m->in, m->kp, 1.0f / m->s_in, m->xq, stream);
   if (rc) return rc;
-  rc = dlq_linear_s8(m->xq, B, m->kp, m->w1, m->hidden, m->a1, m->b1, 1.0f / m->s_hidden, 1,
-                     DLQ_OUT_S8, m->hq, stream);
+  rc = dlq_linear_s8(m->xq, B, m->kp, m->w1, m->hidden, m->a1, m->b1, 1, DLQ_OUT_S8, m->hq, stream);
   if (rc) return rc;
-  return dlq_linear_s8(m->hq, B, m->hidden, m->w2, m->out, m->a2, m->b2, 1.f, 0, DLQ_OUT_F32,
-                       logits, stream);
+  return dlq_linear_s8(m->hq, B, m->hidden, m->w2, m->out, m->a2, m->b2, 0, DLQ_OUT_F32, logits, stream);
 }
 
 int dlq_mlp_copy_hidden(const dlq_mlp* m, int B, int8_t* dst, size_t cap, void* stream) {

@@ -179,8 +179,10 @@ int conv2d_nhwc_s8(const dlq_resnet18* m, const ConvLayer& c, const int8_t* x, i
   dlq_conv_desc d{N, H, W, c.Cstore, c.OC, c.k, c.k, c.s, c.s, c.p, c.p};
   *OH = out_dim(H, c.k, c.s, c.p);
   *OW = out_dim(W, c.k, c.s, c.p);
-  return dlq_conv2d_nhwc_s8(&d, x, c.w, c.alpha, c.beta, residual, res_scale,
-                            inv_scale(m->scales.at(c.site)), relu ? 1 : 0, DLQ_OUT_S8, y, s);
+  // alpha/beta are already in this conv's output-grid units (prepare); the
+  // residual's scale is converted the same way.
+  const float r_s = residual ? dlq::res_scale(res_scale, m->scales.at(c.site)) : 0.f;
+  return dlq_conv2d_nhwc_s8(&d, x, c.w, c.alpha, c.beta, residual, r_s, relu ? 1 : 0, DLQ_OUT_S8, y, s);
 }
 
 // basic_block_forward (infer_e2e.cu:156-203): conv-bn-relu, conv-bn,
@@ -339,7 +341,8 @@ int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
     std::vector<float> alpha(ocp, 0.f), beta(ocp, 0.f);
     fold_bn(m->scales.at(c.in_site), sw.data(), m->tensors.at(c.bn + ".weight").data(),
             m->tensors.at(c.bn + ".bias").data(), m->tensors.at(c.bn + ".running_mean").data(),
-            m->tensors.at(c.bn + ".running_var").data(), 1e-5f, c.OC, alpha.data(), beta.data());
+            m->tensors.at(c.bn + ".running_var").data(), 1e-5f, m->scales.at(c.site), c.OC, alpha.data(),
+            beta.data());
     if ((rc = dev_alloc(m, &c.w, pb)) || (rc = dev_alloc(m, &c.alpha, ocp * 4)) ||
         (rc = dev_alloc(m, &c.beta, ocp * 4)))
       return rc;
@@ -450,7 +453,7 @@ int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, 
   if (rc) return rc;
   m->stage["gap"] = {m->gq, nB * 512};
   if ((rc = mark(m, s))) return rc;
-  rc = dlq_linear_s8(m->gq, B, 512, m->fc_w, 1000, m->fc_alpha, m->fc_beta, 1.f, 0, DLQ_OUT_F32,
+  rc = dlq_linear_s8(m->gq, B, 512, m->fc_w, 1000, m->fc_alpha, m->fc_beta, 0, DLQ_OUT_F32,
                      logits, stream);
   if (rc) return rc;
   if ((rc = mark(m, s))) return rc;

@@ -35,14 +35,15 @@ _SIGS = {
     "dlq_last_error": ([], C.c_char_p),
     "dlq_device_arch": ([_i, C.c_char_p, _i], _i),
     "dlq_quantize_weights_s8": ([_vp, _i, _i, _vp, _vp], _i),
-    "dlq_fold_bn": ([_f, _vp, _vp, _vp, _vp, _vp, _f, _i, _vp, _vp], _i),
+    "dlq_fold_bn": ([_f, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp], _i),
+    "dlq_res_scale": ([_f, _f], _f),
     "dlq_conv_packed_oc": ([_i], _i),
     "dlq_conv_packed_bytes": ([_i, _i, _i, _i], _sz),
     "dlq_pack_conv_weights_s8": ([_vp, _i, _i, _i, _i, _i, _vp], _i),
     "dlq_quantize_nchw_to_nhwc_s8": ([_vp, _i, _i, _i, _i, _i, _f, _vp, _vp], _i),
     "dlq_quantize_rows_s8": ([_vp, _i, _i, _i, _f, _vp, _vp], _i),
-    "dlq_conv2d_nhwc_s8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _i, _vp, _vp], _i),
-    "dlq_linear_s8": ([_vp, _i, _i, _vp, _i, _vp, _vp, _f, _i, _i, _vp, _vp], _i),
+    "dlq_conv2d_nhwc_s8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp], _i),
+    "dlq_linear_s8": ([_vp, _i, _i, _vp, _i, _vp, _vp, _i, _i, _vp, _vp], _i),
     "dlq_maxpool2d_3x3_s2p1_nhwc_s8": ([_vp, _i, _i, _i, _i, _vp, _vp], _i),
     "dlq_gap_nhwc_s8": ([_vp, _i, _i, _i, _f, _vp, _vp], _i),
     "dlq_im2col_nchw_s8": ([_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp], _i),

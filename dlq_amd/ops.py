@@ -36,13 +36,18 @@ def quantize_weights(w: np.ndarray):
     return q, s
 
 
-def fold_bn(s_x: float, s_w, g, b, m, v, eps=1e-5):
+def fold_bn(s_x: float, s_w, g, b, m, v, s_y: float, eps=1e-5):
+    """alpha/beta of the fused epilogue in output-grid units (dlq_fold_bn)."""
     arrs = [np.ascontiguousarray(a, np.float32) for a in (s_w, g, b, m, v)]
     OC = arrs[1].size
     alpha = np.empty(OC, np.float32); beta = np.empty(OC, np.float32)
-    check(lib.dlq_fold_bn(float(s_x), *[ptr(a) for a in arrs], float(eps), OC, ptr(alpha), ptr(beta)),
-          "fold_bn")
+    check(lib.dlq_fold_bn(float(s_x), *[ptr(a) for a in arrs], float(eps), float(s_y), OC, ptr(alpha),
+                          ptr(beta)), "fold_bn")
     return alpha, beta
+
+
+def res_scale(s_r: float, s_y: float) -> float:
+    return lib.dlq_res_scale(float(s_r), float(s_y))
 
 
 def packed_oc(OC: int) -> int:
@@ -95,29 +100,28 @@ def quantize_rows(x: torch.Tensor, scale: float, ld: int) -> torch.Tensor:
 def conv2d_nhwc_s8(x: torch.Tensor, w_packed: torch.Tensor, OC: int, k: int, stride: int, pad: int,
                    alpha: torch.Tensor | None = None, beta: torch.Tensor | None = None,
                    residual: torch.Tensor | None = None, res_scale: float = 0.0,
-                   out_scale: float = 1.0, relu: bool = True, out_kind: int = DLQ_OUT_S8):
-    """Implicit-GEMM int8 conv (+ fused epilogue) on NHWC x[N,H,W,C]."""
+                   relu: bool = True, out_kind: int = DLQ_OUT_S8):
+    """Implicit-GEMM int8 conv (+ fused epilogue) on NHWC x[N,H,W,C]; for int8
+    output alpha/beta/res_scale are in output-grid units (fold_bn, res_scale)."""
     _dev(x, torch.int8)
     N, H, W, Cc = x.shape
     OH, OW = out_dim(H, k, stride, pad), out_dim(W, k, stride, pad)
     dt = {DLQ_OUT_S8: torch.int8, DLQ_OUT_F32: torch.float32, DLQ_OUT_S32: torch.int32}[out_kind]
     y = torch.empty((N, OH, OW, OC), dtype=dt, device=x.device)
     d = ConvDesc(N, H, W, Cc, OC, k, k, stride, stride, pad, pad)
-    inv = float(np.float32(1.0) / np.float32(out_scale))
     check(lib.dlq_conv2d_nhwc_s8(C.byref(d), ptr(x), ptr(w_packed), ptr(alpha), ptr(beta), ptr(residual),
-                                 float(res_scale), inv, int(relu), out_kind, ptr(y), stream_handle()),
+                                 float(res_scale), int(relu), out_kind, ptr(y), stream_handle()),
           "conv2d_nhwc_s8")
     return y
 
 
 def linear_s8(x: torch.Tensor, w_packed: torch.Tensor, OC: int, alpha=None, beta=None,
-              out_scale: float = 1.0, relu: bool = False, out_kind: int = DLQ_OUT_F32):
+              relu: bool = False, out_kind: int = DLQ_OUT_F32):
     _dev(x, torch.int8)
     N, K = x.shape
     dt = {DLQ_OUT_S8: torch.int8, DLQ_OUT_F32: torch.float32, DLQ_OUT_S32: torch.int32}[out_kind]
     y = torch.empty((N, OC), dtype=dt, device=x.device)
-    inv = float(np.float32(1.0) / np.float32(out_scale))
-    check(lib.dlq_linear_s8(ptr(x), N, K, ptr(w_packed), OC, ptr(alpha), ptr(beta), inv, int(relu),
+    check(lib.dlq_linear_s8(ptr(x), N, K, ptr(w_packed), OC, ptr(alpha), ptr(beta), int(relu),
                             out_kind, ptr(y), stream_handle()), "linear_s8")
     return y
 

@@ -61,11 +61,15 @@ int dlq_device_arch(int dev, char* buf, int buflen);
  * scale[o] = max|w[o,:]|/127 (1 if all zero), q = clamp(rne(w/scale), +-127). */
 int dlq_quantize_weights_s8(const float* w, int OC, int K, int8_t* q, float* scale);
 
-/* Dequant * BatchNorm folded into one affine per channel (replaces bn_launch,
- * RK/runtime/infer_e2e.cu:83-97 and RK/kernels/bn_inference.cu:22-27):
- *   t = g/sqrtf(v+eps); alpha = (s_x*s_w)*t; beta = b - m*t.                 */
+/* Dequant * BatchNorm * requant folded into one affine per channel, in units
+ * of the output int8 grid (replaces bn_launch, RK/runtime/infer_e2e.cu:83-97
+ * and RK/kernels/bn_inference.cu:22-27):
+ *   t = g/sqrtf(v+eps); inv = 1/s_y;
+ *   alpha = ((s_x*s_w)*t)*inv; beta = (b - m*t)*inv.                        */
 int dlq_fold_bn(float s_x, const float* s_w, const float* g, const float* b, const float* m,
-                const float* v, float eps, int OC, float* alpha, float* beta);
+                const float* v, float eps, float s_y, int OC, float* alpha, float* beta);
+/* A residual of scale s_r added into an output of scale s_y: s_r*(1/s_y). */
+float dlq_res_scale(float s_r, float s_y);
 
 /* Padded output-channel count the packed weights / alpha / beta must have. */
 int dlq_conv_packed_oc(int OC);
@@ -108,15 +112,16 @@ int dlq_quantize_rows_s8(const float* x, int rows, int cols, int ldy, float inv_
  * sgemm_tiled) followed by bn_launch (:83-97), add_inplace (RK/kernels/add.cu)
  * and relu_forward (RK/kernels/relu.cu) as wired in basic_block_forward
  * (:156-203).  Output NHWC [N][OH][OW][OC]:
- *   DLQ_OUT_S8 : y = fmaf(float(acc), alpha[o], beta[o]);
+ *   DLQ_OUT_S8 : alpha/beta/res_scale in output-grid units (dlq_fold_bn,
+ *                dlq_res_scale):
+ *                y = fmaf(float(acc), alpha[o], beta[o]);
  *                y = fmaf(float(residual), res_scale, y) if residual != NULL;
- *                y = max(y, 0) if relu; out = clamp(rne(y * inv_out_scale), +-127)
+ *                out = rne(clamp(y, relu ? 0 : -127, 127))
  *   DLQ_OUT_F32: out = fmaf(float(acc), alpha[o], beta[o]) (max(.,0) if relu)
  *   DLQ_OUT_S32: out = acc (int32)                                           */
 int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
                        const float* alpha, const float* beta, const int8_t* residual,
-                       float res_scale, float inv_out_scale, int relu, int out_kind, void* y,
-                       void* stream);
+                       float res_scale, int relu, int out_kind, void* y, void* stream);
 
 /* Dense layer on int8 rows: y[N][OC] from x[N][K] (K % 64 == 0) and packed
  * weights [OCp][K]; same epilogue kinds.  Replaces fc_forward
@@ -125,8 +130,7 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
  * matmul_a_b_kernel + bias_forward_kernel + relu_forward_kernel;
  * v5.cu:127-157 cublasSgemm + bias_add_kernel + relu_kernel). */
 int dlq_linear_s8(const int8_t* x, int N, int K, const int8_t* w_packed, int OC, const float* alpha,
-                  const float* beta, float inv_out_scale, int relu, int out_kind, void* y,
-                  void* stream);
+                  const float* beta, int relu, int out_kind, void* y, void* stream);
 
 /* 3x3/s2/p1 max pool on int8 NHWC (RK/kernels/maxpool2d.cu:4-41, launched at
  * RK/runtime/infer_e2e.cu:283-293; out-of-bounds taps skipped). */

@@ -193,19 +193,27 @@ ORA_API void ora_quantize_weights_s8(const float* w, int OC, int K, int8_t* q, f
   }
 }
 
-/* Fold dequant and BN (kernels/bn_inference.cu:22-27) into one affine per
- * output channel:  t = g/sqrtf(v+eps);  alpha = (s_x*s_w)*t;  beta = b - m*t. */
+/* Fold dequant, BN (kernels/bn_inference.cu:22-27) and the output requant
+ * scale into one affine per output channel, in units of the output int8 grid:
+ *   t = g/sqrtf(v+eps);  inv_y = 1/s_y;
+ *   alpha = ((s_x*s_w)*t)*inv_y;  beta = (b - m*t)*inv_y. */
 ORA_API void ora_fold_bn(float s_x, const float* s_w, const float* g, const float* b,
-                         const float* m, const float* v, float eps, int OC, float* alpha,
-                         float* beta) {
+                         const float* m, const float* v, float eps, float s_y, int OC,
+                         float* alpha, float* beta) {
+  const float inv_y = 1.0f / s_y;
   for (int o = 0; o < OC; ++o) {
     const float t = g[o] / sqrtf(v[o] + eps);
     const float sxw = s_x * s_w[o];
-    alpha[o] = sxw * t;
+    const float a = sxw * t;
+    alpha[o] = a * inv_y;
     const float mt = m[o] * t;
-    beta[o] = b[o] - mt;
+    const float bb = b[o] - mt;
+    beta[o] = bb * inv_y;
   }
 }
+
+/* Residual scale in output-grid units: s_r * (1/s_y). */
+ORA_API float ora_res_scale(float s_r, float s_y) { return s_r * (1.0f / s_y); }
 
 /* fp32 -> int8 with one per-tensor scale: q = sat(rne(x * inv_s)). */
 ORA_API void ora_quantize_f32_s8(const float* x, size_t n, float inv_s, int8_t* q) {
@@ -263,22 +271,24 @@ ORA_API int ora_conv2d_nchw_s8_acc(const int8_t* x, int N, int IC, int H, int W,
 }
 
 /* Fused epilogue (replaces bn_inference + add_inplace + relu_forward,
- * infer_e2e.cu:168-200) on NCHW accumulators:
+ * infer_e2e.cu:168-200) on NCHW accumulators, alpha/beta/r_s already in
+ * output-grid units (ora_fold_bn, ora_res_scale):
  *   y = fmaf(float(acc), alpha[c], beta[c])
- *   y = fmaf(float(res), s_r, y)          if res != NULL
- *   y = max(y, 0)                         if relu
- *   q = sat(rne(y * inv_s))                                            */
+ *   y = fmaf(float(res), r_s, y)            if res != NULL
+ *   q = rne(clamp(y, relu ? 0 : -127, 127))                              */
 ORA_API void ora_epilogue_s8(const int32_t* acc, int N, int OC, int HW, const float* alpha,
-                             const float* beta, const int8_t* res, float s_r, int relu,
-                             float inv_s, int8_t* out) {
+                             const float* beta, const int8_t* res, float r_s, int relu,
+                             int8_t* out) {
+  const float lo = relu ? 0.f : -127.f;
   for (int n = 0; n < N; ++n)
     for (int c = 0; c < OC; ++c)
       for (int i = 0; i < HW; ++i) {
         const size_t idx = ((size_t)n * OC + c) * HW + i;
         float y = fmaf((float)acc[idx], alpha[c], beta[c]);
-        if (res) y = fmaf((float)res[idx], s_r, y);
-        if (relu) y = y > 0.f ? y : 0.f;
-        out[idx] = sat_rne(y * inv_s);
+        if (res) y = fmaf((float)res[idx], r_s, y);
+        y = y < lo ? lo : y;
+        y = y > 127.f ? 127.f : y;
+        out[idx] = (int8_t)(int)rintf(y);
       }
 }
 

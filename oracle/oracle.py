@@ -38,12 +38,13 @@ _SIGS = {
     "ora_conv2d_f32": [_f32p, _i, _i, _i, _f32p, _i, _i, _i, _i, _i, _i, _i, _f32p, _f32p],
     "ora_mlp_layer_f32": [_f32p, _f32p, _f32p, _i, _i, _i, _i, _f32p],
     "ora_quantize_weights_s8": [_f32p, _i, _i, _s8p, _f32p],
-    "ora_fold_bn": [_f, _f32p, _f32p, _f32p, _f32p, _f32p, _f, _i, _f32p, _f32p],
+    "ora_fold_bn": [_f, _f32p, _f32p, _f32p, _f32p, _f32p, _f, _f, _i, _f32p, _f32p],
+    "ora_res_scale": [_f, _f],
     "ora_quantize_f32_s8": [_f32p, C.c_size_t, _f, _s8p],
     "ora_im2col_nchw_s8": [_s8p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _s8p],
     "ora_gemm_s8s8s32": [_s8p, _s8p, _s32p, _i, _i, _i],
     "ora_conv2d_nchw_s8_acc": [_s8p, _i, _i, _i, _i, _s8p, _i, _i, _i, _i, _i, _i, _i, _s32p],
-    "ora_epilogue_s8": [_s32p, _i, _i, _i, _f32p, _f32p, C.c_void_p, _f, _i, _f, _s8p],
+    "ora_epilogue_s8": [_s32p, _i, _i, _i, _f32p, _f32p, C.c_void_p, _f, _i, _s8p],
     "ora_epilogue_f32": [_s32p, _i, _i, _i, _f32p, _f32p, _i, _f32p],
     "ora_maxpool_s8": [_s8p, _i, _i, _i, _i, _s8p],
     "ora_gap_s8": [_s8p, _i, _i, _i, _f, C.c_void_p, _s8p],
@@ -62,7 +63,7 @@ def lib():
         for name, args in _SIGS.items():
             fn = getattr(L, name)
             fn.argtypes = args
-            fn.restype = C.c_int if name == "ora_conv2d_nchw_s8_acc" else None
+            fn.restype = {"ora_conv2d_nchw_s8_acc": C.c_int, "ora_res_scale": C.c_float}.get(name)
         _LIB = L
     return _LIB
 
@@ -190,12 +191,17 @@ def quantize_weights_s8(w):
     return q, s
 
 
-def fold_bn(s_x, s_w, bn, eps=1e-5):
+def fold_bn(s_x, s_w, bn, s_y, eps=1e-5):
+    """alpha, beta of the fused epilogue in output-grid units (ora_fold_bn)."""
     g, b, m, v = (_c(t, np.float32) for t in bn)
     OC = g.size
     alpha = np.empty(OC, np.float32); beta = np.empty(OC, np.float32)
-    lib().ora_fold_bn(np.float32(s_x), _c(s_w, np.float32), g, b, m, v, eps, OC, alpha, beta)
+    lib().ora_fold_bn(np.float32(s_x), _c(s_w, np.float32), g, b, m, v, eps, np.float32(s_y), OC, alpha, beta)
     return alpha, beta
+
+
+def res_scale(s_r, s_y):
+    return np.float32(lib().ora_res_scale(np.float32(s_r), np.float32(s_y)))
 
 
 def inv_scale(s):
@@ -220,12 +226,13 @@ def conv_s8_acc(x, wq, stride, pad):
     return acc
 
 
-def epilogue_s8(acc, alpha, beta, s_out, res=None, s_res=0.0, relu=True):
+def epilogue_s8(acc, alpha, beta, res=None, r_s=0.0, relu=True):
+    """int8 epilogue with alpha/beta/r_s in output-grid units (fold_bn, res_scale)."""
     N, OC = acc.shape[:2]; HW = int(np.prod(acc.shape[2:]))
     out = np.empty(acc.shape, np.int8)
     r = None if res is None else _c(res, np.int8)
     lib().ora_epilogue_s8(_c(acc, np.int32), N, OC, HW, _c(alpha, np.float32), _c(beta, np.float32),
-                          _ptr(r), np.float32(s_res), int(relu), inv_scale(s_out), out)
+                          _ptr(r), np.float32(r_s), int(relu), out)
     return out
 
 
@@ -258,6 +265,14 @@ def fc_s8(x, wq, alpha, beta):
     return out, accs
 
 
+def mlp_alpha_beta(s_x, s_w, bias, s_y):
+    """Hidden-layer epilogue constants in output-grid units (mlp.cpp prep_layer):
+    alpha = (s_x*s_w)*(1/s_y), beta = bias*(1/s_y), fp32 in this order."""
+    inv = np.float32(np.float32(1.0) / np.float32(s_y))
+    sa = (np.float32(s_x) * _c(s_w, np.float32)).astype(np.float32)
+    return (sa * inv).astype(np.float32), (_c(bias, np.float32) * inv).astype(np.float32)
+
+
 def fc_alpha(s_x, s_w):
     return (np.float32(s_x) * _c(s_w, np.float32)).astype(np.float32)
 
@@ -273,10 +288,11 @@ def resnet18_forward_s8(sd, scales, x, eps=1e-5):
 
     def conv(name, xin, s_in, w, bn, stride, pad, res=None, s_res=0.0, relu=True):
         wq, sw = quantize_weights_s8(w)
-        alpha, beta = fold_bn(s_in, sw, bn, eps)
+        alpha, beta = fold_bn(s_in, sw, bn, scales[name], eps)
         acc = conv_s8_acc(xin, wq, stride, pad)
         dumps[name + ".acc"] = acc
-        out = epilogue_s8(acc, alpha, beta, scales[name], res, s_res, relu=relu)
+        r_s = res_scale(s_res, scales[name]) if res is not None else 0.0
+        out = epilogue_s8(acc, alpha, beta, res, r_s, relu=relu)
         dumps[name] = out
         return out
 

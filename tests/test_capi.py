@@ -48,9 +48,10 @@ def test_host_quantize_and_fold_match_oracle():
         q_lib, s_lib = ops.quantize_weights(w)
         q_ora, s_ora = O.quantize_weights_s8(w)
         assert np.array_equal(q_lib, q_ora) and np.array_equal(s_lib, s_ora)
-        a_lib, b_lib = ops.fold_bn(0.0123, s_lib, *bn)
-        a_ora, b_ora = O.fold_bn(0.0123, s_ora, bn)
+        a_lib, b_lib = ops.fold_bn(0.0123, s_lib, *bn, 0.047)
+        a_ora, b_ora = O.fold_bn(0.0123, s_ora, bn, 0.047)
         assert np.array_equal(a_lib, a_ora) and np.array_equal(b_lib, b_ora)
+        assert np.float32(ops.res_scale(0.052, 0.047)) == O.res_scale(0.052, 0.047)
 
 
 def test_pack_layout():
@@ -80,7 +81,7 @@ def test_pack_layout():
 def test_errors_are_returned_not_exited():
     from dlq_amd.lib import ConvDesc, lib
     d = ConvDesc(1, 8, 8, 3, 8, 3, 3, 1, 1, 1, 1)  # C=3 with a 3x3 kernel: unsupported
-    rc = lib.dlq_conv2d_nhwc_s8(C.byref(d), 1, 1, 1, 1, None, 0.0, 1.0, 1, 0, 1, None)
+    rc = lib.dlq_conv2d_nhwc_s8(C.byref(d), 1, 1, 1, 1, None, 0.0, 1, 0, 1, None)
     assert rc == 1 and b"unsupported" in lib.dlq_last_error()
     assert lib.dlq_conv_packed_bytes(8, 3, 3, 3) == 0
     h = C.c_void_p()

@@ -79,18 +79,18 @@ def test_conv_fused_epilogue_bitexact(gpu, shape, residual):
     w, bn = rand_conv(rng, OC, IC, k)
     wq, sw = O.quantize_weights_s8(w)
     s_x, s_y, s_r = 0.031, 0.047, 0.052
-    alpha, beta = O.fold_bn(s_x, sw, bn)
+    alpha, beta = O.fold_bn(s_x, sw, bn, s_y)
+    r_s = O.res_scale(s_r, s_y)
     acc = O.conv_s8_acc(x, wq, s, p)
     res = rand_s8(rng, acc.shape) if residual else None
     relu = (k != 1)  # downsample convs have no ReLU (infer_e2e.cu:187-196)
-    ref = O.epilogue_s8(acc, alpha, beta, s_y, res, s_r, relu)
+    ref = O.epilogue_s8(acc, alpha, beta, res, r_s, relu)
     xd, wd = _gpu_conv_inputs(x, wq, k)
     ocp = ops.packed_oc(OC)
-    a_alpha, a_beta = ops.fold_bn(s_x, sw, *bn)
+    a_alpha, a_beta = ops.fold_bn(s_x, sw, *bn, s_y)
     assert np.array_equal(a_alpha, alpha) and np.array_equal(a_beta, beta)  # host prep == oracle
     y = ops.conv2d_nhwc_s8(xd, wd, OC, k, s, p, _cuda(ops.pad_vec(a_alpha, ocp)), _cuda(ops.pad_vec(a_beta, ocp)),
-                           residual=_cuda(nchw_to_nhwc(res)) if residual else None, res_scale=s_r,
-                           out_scale=s_y, relu=relu)
+                           residual=_cuda(nchw_to_nhwc(res)) if residual else None, res_scale=r_s, relu=relu)
     got = nhwc_to_nchw(y.cpu().numpy())
     assert np.array_equal(got, ref), f"{name}: {np.count_nonzero(got != ref)} int8 mismatches"
 
@@ -222,7 +222,8 @@ def test_mnist_mlp_bitexact(gpu, hidden):
     q2, sw2 = O.quantize_weights_s8(W2.T.copy())
     acc1 = np.empty((1024, hidden), np.int32)
     O.lib().ora_mlp_layer_s8_acc(xq, q1.T.copy(), 1024, 784, hidden, acc1)
-    h = O.epilogue_s8(acc1[:, :, None], O.fc_alpha(s_in, sw1), b1, s_h, relu=True)[:, :, 0]
+    a1, bb1 = O.mlp_alpha_beta(s_in, sw1, b1, s_h)
+    h = O.epilogue_s8(acc1[:, :, None], a1, bb1, relu=True)[:, :, 0]
     acc2 = np.empty((1024, 10), np.int32)
     O.lib().ora_mlp_layer_s8_acc(h, q2.T.copy(), 1024, hidden, 10, acc2)
     ref = np.empty((1024, 10), np.float32)

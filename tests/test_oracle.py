@@ -132,21 +132,34 @@ def test_conv_s8_acc_vs_numpy():
 
 
 def test_epilogue_s8_sequence():
-    """The fp32 epilogue is exactly: fma, fma(residual), relu, x*inv, rne, clamp."""
+    """The fp32 epilogue is exactly: fma, fma(residual), clamp to [0 or -127, 127], rne."""
     rng = np.random.default_rng(5)
     acc = rng.integers(-200000, 200000, size=(2, 8, 30), dtype=np.int32)
-    alpha = (rng.random(8, dtype=np.float32) * 1e-3).astype(np.float32)
-    beta = (rng.standard_normal(8, dtype=np.float32) * 0.1).astype(np.float32)
+    alpha = (rng.random(8, dtype=np.float32) * 1e-2).astype(np.float32)
+    beta = (rng.standard_normal(8, dtype=np.float32) * 3).astype(np.float32)
     res = rand_s8(rng, acc.shape)
-    s_y, s_r = np.float32(0.05), np.float32(0.07)
-    out = O.epilogue_s8(acc, alpha, beta, s_y, res, s_r, relu=True)
-    a64, al, be = acc.astype(np.float32).astype(np.float64), alpha[None, :, None].astype(np.float64), beta[None, :, None]
-    y = (a64 * al + be).astype(np.float32)  # exact product + one rounding == fmaf (|products| < 2^53)
-    y = (res.astype(np.float64) * np.float64(s_r) + y).astype(np.float32)
-    y = np.maximum(y, np.float32(0))
-    inv = np.float32(np.float32(1) / s_y)
-    ref = np.clip(np.rint((y * inv).astype(np.float32)), -127, 127).astype(np.int8)
-    assert np.array_equal(out, ref)
+    r_s = np.float32(1.4)
+    for relu in (True, False):
+        out = O.epilogue_s8(acc, alpha, beta, res, r_s, relu=relu)
+        a64 = acc.astype(np.float32).astype(np.float64)
+        y = (a64 * alpha[None, :, None].astype(np.float64) + beta[None, :, None]).astype(np.float32)  # == fmaf
+        y = (res.astype(np.float64) * np.float64(r_s) + y).astype(np.float32)
+        ref = np.rint(np.clip(y, 0 if relu else -127, 127)).astype(np.int8)
+        assert np.array_equal(out, ref)
+        assert (out.min() >= 0) == relu
+
+
+def test_fold_bn_output_grid():
+    """alpha/beta fold dequant, BN and the 1/s_y requant in a fixed fp32 order."""
+    rng = np.random.default_rng(8)
+    _, (g, b, m, v) = rand_conv(rng, 16, 4, 3)
+    s_w = (rng.random(16, dtype=np.float32) * 0.01).astype(np.float32)
+    a, bb = O.fold_bn(0.02, s_w, (g, b, m, v), 0.05)
+    f = np.float32
+    t = (g / np.sqrt((v + f(1e-5)).astype(f)).astype(f)).astype(f)
+    inv = f(f(1) / f(0.05))
+    assert np.array_equal(a, (((f(0.02) * s_w).astype(f) * t).astype(f) * inv).astype(f))
+    assert np.array_equal(bb, ((b - (m * t).astype(f)).astype(f) * inv).astype(f))
 
 
 def test_gap_and_maxpool_s8():

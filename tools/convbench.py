@@ -49,7 +49,7 @@ def main():
         OH = ops.out_dim(H, k, s, p)
         r = torch.randint(-127, 128, (args.batch, OH, OH, OC), dtype=torch.int8, device="cuda") if res else None
         f = lambda: ops.conv2d_nhwc_s8(x, w, OC, k, s, p, alpha, beta, residual=r, res_scale=0.01,  # noqa: E731
-                                       out_scale=0.05, relu=True)
+                                       relu=True)
         for _ in range(3):
             f()
         torch.cuda.synchronize()
