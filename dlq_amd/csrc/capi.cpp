@@ -204,6 +204,25 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d launch: ") + hipGetErrorString(e));
 }
 
+size_t dlq_stem_packed_bytes(void) { return stem_packed_bytes(); }
+
+int dlq_pack_stem_weights_s8(const int8_t* q_oihw, int8_t* packed) {
+  if (!q_oihw || !packed) return fail(DLQ_ERR_ARG, "pack_stem_weights: null");
+  pack_stem_weights(q_oihw, packed);
+  return DLQ_OK;
+}
+
+int dlq_stem_fused_s8(const float* x, int N, const int8_t* w_stem, const float* alpha, const float* beta,
+                      float inv_s, int8_t* y, void* stream) {
+  if (N < 0) return fail(DLQ_ERR_ARG, "stem_fused: bad batch");
+  if (N == 0) return DLQ_OK;
+  if (!x || !w_stem || !alpha || !beta || !y) return fail(DLQ_ERR_ARG, "stem_fused: null pointer");
+  if ((long long)N * 3 * 224 * 224 * 4 >= (1LL << 31) * 4LL)
+    return fail(DLQ_ERR_ARG, "stem_fused: batch too large");
+  hipError_t e = launch_stem_fused(x, N, w_stem, alpha, beta, inv_s, y, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("stem_fused launch: ") + hipGetErrorString(e));
+}
+
 int dlq_linear_s8(const int8_t* x, int N, int K, const int8_t* w_packed, int OC, const float* alpha,
                   const float* beta, int relu, int out_kind, void* y, void* stream) {
   if (K <= 0 || K % 64) return fail(DLQ_ERR_ARG, "linear: K must be a positive multiple of 64");

@@ -40,6 +40,11 @@ bool is_stem(int C, int kH, int kW);
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s);
 bool conv3x3s1_supported(const ConvArgs& a);
 hipError_t launch_conv3x3s1(const ConvArgs& a, hipStream_t s);
+// Fused stem (stem.hip): quantise + conv1 7x7/s2 + BN/ReLU/requant + maxpool.
+size_t stem_packed_bytes();
+void pack_stem_weights(const int8_t* q_oihw, int8_t* out);
+hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float* alpha, const float* beta,
+                             float inv_s, int8_t* y, hipStream_t s);
 hipError_t launch_quantize_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cout,
                                         float inv_s, int8_t* y, hipStream_t s);
 hipError_t launch_quantize_rows(const float* x, int rows, int cols, int ldy, float inv_s,

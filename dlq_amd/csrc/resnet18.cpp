@@ -13,6 +13,7 @@
 // :280, :292, :423); the batch dimension is honoured; BN, ReLU, residual add
 // and requantisation run in the conv kernel's epilogue.
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -55,6 +56,7 @@ struct dlq_resnet18 {
   std::vector<ConvLayer> convs;
   std::vector<Block> blocks;
   int stem = -1;
+  int8_t* stem_w = nullptr;  // fused-stem weight image (dlq_pack_stem_weights_s8)
   // FC
   int8_t* fc_w = nullptr;
   float* fc_alpha = nullptr;
@@ -163,13 +165,23 @@ void free_all(dlq_resnet18* m) {
   m->allocs.clear();
   for (auto& c : m->convs) { c.w = nullptr; c.alpha = nullptr; c.beta = nullptr; }
   m->fc_w = nullptr; m->fc_alpha = m->fc_beta = nullptr;
-  m->xq = m->c1 = m->gq = nullptr;
+  m->xq = m->c1 = m->gq = m->stem_w = nullptr;
   for (auto& b : m->buf) b = nullptr;
   m->keepbuf.clear();
   m->prepared = false;
 }
 
 float inv_scale(float s) { return 1.0f / s; }
+
+// DLQ_STEM_UNFUSED=1 runs quantise / conv1 / maxpool as three launches
+// (A/B timing, and exposes the "input_q" and "conv1" stages).
+bool unfused_stem() {
+  static const bool v = [] {
+    const char* e = std::getenv("DLQ_STEM_UNFUSED");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 
 // conv2d_nchw_im2col_gemm + bn_launch (+ add_inplace + relu_forward) of the
 // reference, as one implicit-GEMM launch with the epilogue fused.
@@ -351,6 +363,13 @@ int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
         (e = hipMemcpy(c.alpha, alpha.data(), ocp * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c.beta, beta.data(), ocp * 4, hipMemcpyHostToDevice)) != hipSuccess)
       return hip_fail(e, "weight upload");
+    if (&c == &m->convs[m->stem]) {  // the fused stem's space-to-depth weight image
+      std::vector<int8_t> sp(stem_packed_bytes());
+      pack_stem_weights(q.data(), sp.data());
+      if ((rc = dev_alloc(m, &m->stem_w, sp.size()))) return rc;
+      if ((e = hipMemcpy(m->stem_w, sp.data(), sp.size(), hipMemcpyHostToDevice)) != hipSuccess)
+        return hip_fail(e, "stem weight upload");
+    }
   }
   {  // FC: int8 [1000][512] per-row scales; logits = fmaf(acc, s_gap*s_w[o], bias[o])
     const int O = 1000, I = 512, op = packed_oc(O);
@@ -377,8 +396,9 @@ int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
   }
   // Workspace (int8 NHWC), sized once for max_batch.
   const size_t B = (size_t)max_batch;
-  if ((rc = dev_alloc(m, &m->xq, B * 224 * 224 * kStemC)) ||
-      (rc = dev_alloc(m, &m->c1, B * 112 * 112 * 64)) || (rc = dev_alloc(m, &m->gq, B * 512)))
+  if ((rc = dev_alloc(m, &m->gq, B * 512))) return rc;
+  if (unfused_stem() &&
+      ((rc = dev_alloc(m, &m->xq, B * 224 * 224 * kStemC)) || (rc = dev_alloc(m, &m->c1, B * 112 * 112 * 64))))
     return rc;
   for (auto& b : m->buf)
     if ((rc = dev_alloc(m, &b, B * 56 * 56 * 64))) return rc;
@@ -410,23 +430,30 @@ int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, 
   const size_t nB = (size_t)B;
   int rc;
   m->stage.clear();
-  // 0) input quantisation (fp32 NCHW -> int8 NHWC4)
-  rc = dlq_quantize_nchw_to_nhwc_s8(x, B, 3, 224, 224, kStemC, inv_scale(m->scales.at("input")), m->xq, stream);
-  if (rc) return rc;
-  m->stage["input_q"] = {m->xq, nB * 224 * 224 * kStemC};
-  // 1) stem conv 7x7/s2 + BN + ReLU (infer_e2e.cu:259-280)
-  int H, W;
-  if ((rc = mark(m, s))) return rc;
-  rc = conv2d_nhwc_s8(m, m->convs[m->stem], m->xq, B, 224, 224, nullptr, 0.f, true, m->c1, s, &H, &W);
-  if (rc) return rc;
-  if ((rc = mark(m, s))) return rc;
-  m->stage["conv1"] = {m->c1, nB * H * W * 64};
-  // maxpool 3x3/s2/p1 (:282-293)
+  int H = 56, W = 56;
   int8_t* cur = m->buf[0];
-  rc = dlq_maxpool2d_3x3_s2p1_nhwc_s8(m->c1, B, 64, H, W, cur, stream);
-  if (rc) return rc;
-  H = out_dim(H, 3, 2, 1);
-  W = out_dim(W, 3, 2, 1);
+  const ConvLayer& st = m->convs[m->stem];
+  if (!unfused_stem()) {
+    // 0+1) fused stem: quantise + conv 7x7/s2 + BN + ReLU + maxpool 3x3/s2
+    //      (infer_e2e.cu:255-293) in one launch
+    if ((rc = mark(m, s))) return rc;
+    rc = dlq_stem_fused_s8(x, B, m->stem_w, st.alpha, st.beta, inv_scale(m->scales.at("input")), cur, stream);
+    if (rc) return rc;
+    if ((rc = mark(m, s))) return rc;
+  } else {
+    // unfused reference sequence (A/B and parity of the fused kernel)
+    rc = dlq_quantize_nchw_to_nhwc_s8(x, B, 3, 224, 224, kStemC, inv_scale(m->scales.at("input")), m->xq, stream);
+    if (rc) return rc;
+    m->stage["input_q"] = {m->xq, nB * 224 * 224 * kStemC};
+    int CH, CW;
+    if ((rc = mark(m, s))) return rc;
+    rc = conv2d_nhwc_s8(m, st, m->xq, B, 224, 224, nullptr, 0.f, true, m->c1, s, &CH, &CW);
+    if (rc) return rc;
+    if ((rc = mark(m, s))) return rc;
+    m->stage["conv1"] = {m->c1, nB * CH * CW * 64};
+    rc = dlq_maxpool2d_3x3_s2p1_nhwc_s8(m->c1, B, 64, CH, CW, cur, stream);
+    if (rc) return rc;
+  }
   if ((rc = record_stage(m, "stem_pool", cur, nB * H * W * 64, s))) return rc;
   // 2-5) layer1..layer4 (:300-415)
   if ((rc = mark(m, s))) return rc;

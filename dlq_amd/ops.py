@@ -65,6 +65,16 @@ def pack_conv_weights(q_oihw: np.ndarray, C_store: int) -> np.ndarray:
     return out
 
 
+def pack_stem_weights(q_oihw: np.ndarray) -> np.ndarray:
+    """conv1 weights [64][3][7][7] int8 -> the fused stem's space-to-depth image."""
+    q = np.ascontiguousarray(q_oihw, np.int8)
+    if q.shape != (64, 3, 7, 7):
+        raise ValueError(f"stem weights must be [64,3,7,7], got {q.shape}")
+    out = np.empty(lib.dlq_stem_packed_bytes(), np.int8)
+    check(lib.dlq_pack_stem_weights_s8(ptr(q), ptr(out)), "pack_stem_weights")
+    return out
+
+
 def pad_vec(v, n):
     out = np.zeros(n, np.float32)
     out[: len(v)] = v
@@ -112,6 +122,21 @@ def conv2d_nhwc_s8(x: torch.Tensor, w_packed: torch.Tensor, OC: int, k: int, str
     check(lib.dlq_conv2d_nhwc_s8(C.byref(d), ptr(x), ptr(w_packed), ptr(alpha), ptr(beta), ptr(residual),
                                  float(res_scale), int(relu), out_kind, ptr(y), stream_handle()),
           "conv2d_nhwc_s8")
+    return y
+
+
+def stem_fused_s8(x: torch.Tensor, w_stem: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor,
+                  in_scale: float) -> torch.Tensor:
+    """quantise + conv1 7x7/s2 + BN/ReLU/requant + maxpool 3x3/s2 in one launch:
+    fp32 NCHW [N,3,224,224] -> int8 NHWC [N,56,56,64] (alpha/beta in conv1's grid)."""
+    _dev(x, torch.float32)
+    N = x.shape[0]
+    if tuple(x.shape[1:]) != (3, 224, 224):
+        raise ValueError(f"stem input must be [N,3,224,224], got {tuple(x.shape)}")
+    y = torch.empty((N, 56, 56, 64), dtype=torch.int8, device=x.device)
+    inv = float(np.float32(1.0) / np.float32(in_scale))
+    check(lib.dlq_stem_fused_s8(ptr(x), N, ptr(w_stem), ptr(alpha), ptr(beta), inv, ptr(y), stream_handle()),
+          "stem_fused_s8")
     return y
 
 

@@ -123,6 +123,19 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
                        const float* alpha, const float* beta, const int8_t* residual,
                        float res_scale, int relu, int out_kind, void* y, void* stream);
 
+/* Fused stem: fp32 NCHW x[N][3][224][224] -> int8 NHWC y[N][56][56][64] =
+ * maxpool3x3s2p1(requant(ReLU(BN(conv7x7s2p3(quant(x)))))).  One launch
+ * replaces the input upload + conv1 + bn1 + relu + maxpool sequence of
+ * RK/runtime/infer_e2e.cu:255-293; the 112x112 conv1 output never reaches
+ * HBM.  w_stem = dlq_pack_stem_weights_s8 image (64 x 256 B: 7x7x3 taps
+ * re-indexed for a 2x2 space-to-depth input), alpha/beta[64] in conv1's
+ * output-grid units, inv_s = 1/input scale.  Bit-identical to
+ * dlq_quantize_nchw_to_nhwc_s8 + dlq_conv2d_nhwc_s8 (stem) + maxpool. */
+size_t dlq_stem_packed_bytes(void);
+int dlq_pack_stem_weights_s8(const int8_t* q_oihw, int8_t* packed);
+int dlq_stem_fused_s8(const float* x, int N, const int8_t* w_stem, const float* alpha, const float* beta,
+                      float inv_s, int8_t* y, void* stream);
+
 /* Dense layer on int8 rows: y[N][OC] from x[N][K] (K % 64 == 0) and packed
  * weights [OCp][K]; same epilogue kinds.  Replaces fc_forward
  * (RK/runtime/infer_e2e.cu:206-219: sgemm_tiled M=1000,N=1,K=512 + host bias)

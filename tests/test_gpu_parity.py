@@ -95,6 +95,27 @@ def test_conv_fused_epilogue_bitexact(gpu, shape, residual):
     assert np.array_equal(got, ref), f"{name}: {np.count_nonzero(got != ref)} int8 mismatches"
 
 
+@pytest.mark.parametrize("N", [1, 3])
+def test_stem_fused_bitexact(gpu, N):
+    """quantise + conv1 7x7/s2 + BN/ReLU/requant + maxpool as ONE launch
+    (infer_e2e.cu:259-301) == the oracle's four separate steps."""
+    from dlq_amd import ops
+    rng = np.random.default_rng(41 + N)
+    x = (rng.standard_normal((N, 3, 224, 224), dtype=np.float32) * 1.7).astype(np.float32)
+    x[0, :, 0, :6] = [[0.5, 1.5, -2.5, 1e9, -1e9, 0.0]] * 3  # ties, saturation, the padded border
+    x[N - 1, 2, 223, 218:] = [-0.5, 2.5, 1e9, -1e9, 3.5, 0.0]
+    w, bn = rand_conv(rng, 64, 3, 7)
+    wq, sw = O.quantize_weights_s8(w)
+    s_in, s_y = 2.64 / 127, 0.043
+    alpha, beta = O.fold_bn(s_in, sw, bn, s_y)
+    xq = O.quantize_f32_s8(x, s_in)
+    ref = O.maxpool_s8(O.epilogue_s8(O.conv_s8_acc(xq, wq, 2, 3), alpha, beta, None, 0.0, True))
+    wst = _cuda(ops.pack_stem_weights(wq))
+    y = ops.stem_fused_s8(_cuda(x), wst, _cuda(alpha), _cuda(beta), s_in)
+    got = nhwc_to_nchw(y.cpu().numpy())
+    assert np.array_equal(got, ref), f"{np.count_nonzero(got != ref)} int8 mismatches"
+
+
 def test_fc_logits_bitexact(gpu):
     from dlq_amd import ops
     from dlq_amd.lib import DLQ_OUT_F32, DLQ_OUT_S32
@@ -173,7 +194,7 @@ def test_resnet18_end_to_end_bitexact(gpu):
     model = ResNet18Int8(sd, scales, max_batch=4, keep_stages=True)
     logits = model(_cuda(x)).cpu().numpy()
     torch.cuda.synchronize()
-    for st in ("conv1", "stem_pool", "layer1", "layer2", "layer3", "layer4", "gap"):
+    for st in ("stem_pool", "layer1", "layer2", "layer3", "layer4", "gap"):
         got = _stage_nchw(model, st, 2)
         assert np.array_equal(got, dumps[st]), f"stage {st}: {np.count_nonzero(got != dumps[st])} mismatches"
     assert np.array_equal(logits.view(np.int32), ref_logits.view(np.int32))

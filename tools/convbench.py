@@ -28,6 +28,20 @@ LAYERS = [
 ]
 
 
+def bench(name, f, iters, tag, macs):
+    for _ in range(3):
+        f()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        f()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / iters
+    print(f"{tag:16s} {name:8s} {us:8.1f} us  {2 * macs / us / 1e6:7.1f} TOPS", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
@@ -36,6 +50,14 @@ def main():
     args = ap.parse_args()
     rng = np.random.default_rng(0)
     tag = f"v1={os.environ.get('DLQ_CONV_V1', '0')} dbg={os.environ.get('DLQ_DBG', '0')}"
+    if "stemf" in args.only.split(","):
+        x = torch.randn(args.batch, 3, 224, 224, device="cuda")
+        q = rng.integers(-127, 128, size=(64, 3, 7, 7), dtype=np.int8)
+        w = torch.from_numpy(ops.pack_stem_weights(q)).cuda()
+        alpha = torch.full((64,), 1e-3, device="cuda")
+        beta = torch.zeros(64, device="cuda")
+        bench("stemf", lambda: ops.stem_fused_s8(x, w, alpha, beta, 0.02), args.iters, tag,
+              args.batch * 112 * 112 * 64 * 3 * 49)
     for name, IC, OC, k, s, p, H, res in LAYERS:
         if args.only and name not in args.only.split(","):
             continue
@@ -50,18 +72,7 @@ def main():
         r = torch.randint(-127, 128, (args.batch, OH, OH, OC), dtype=torch.int8, device="cuda") if res else None
         f = lambda: ops.conv2d_nhwc_s8(x, w, OC, k, s, p, alpha, beta, residual=r, res_scale=0.01,  # noqa: E731
                                        relu=True)
-        for _ in range(3):
-            f()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(args.iters):
-            f()
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / args.iters
-        macs = args.batch * OH * OH * OC * IC * k * k
-        print(f"{tag:16s} {name:8s} {us:8.1f} us  {2 * macs / us / 1e6:7.1f} TOPS", flush=True)
+        bench(name, f, args.iters, tag, args.batch * OH * OH * OC * IC * k * k)
 
 
 if __name__ == "__main__":
