@@ -104,6 +104,27 @@ void pack_conv_weights(const int8_t* q, int OC, int IC, int kH, int kW, int C, i
           out[packed_offset(o, kh * kW + kw, c, OCp, taps)] = q[(((size_t)o * IC + c) * kH + kh) * kW + kw];
 }
 
+bool wide_layout(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW) {
+  static const bool force_v1 = [] {
+    const char* e = std::getenv("DLQ_CONV_V1");
+    return e && e[0] == '1';
+  }();
+  return !force_v1 && conv3x3w_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW);
+}
+
+size_t packed_bytes_for(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW) {
+  if (wide_layout(C, OC, H, W, kH, kW, sH, sW, pH, pW)) return conv3x3w_packed_bytes(OC, C);
+  return packed_bytes(OC, C, kH, kW);
+}
+
+void pack_conv_weights_for(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW,
+                           const int8_t* q, int IC, int8_t* out) {
+  if (wide_layout(C, OC, H, W, kH, kW, sH, sW, pH, pW))
+    conv3x3w_pack(q, OC, IC, C, out);
+  else
+    pack_conv_weights(q, OC, IC, kH, kW, C, out);
+}
+
 }  // namespace dlq
 
 using namespace dlq;
@@ -139,12 +160,14 @@ float dlq_res_scale(float s_r, float s_y) { return res_scale(s_r, s_y); }
 
 int dlq_conv_packed_oc(int OC) { return OC > 0 ? packed_oc(OC) : 0; }
 
-size_t dlq_conv_packed_bytes(int OC, int C, int kH, int kW) { return packed_bytes(OC, C, kH, kW); }
+#define DLQ_DESC_GEOM(d) (d)->C, (d)->OC, (d)->H, (d)->W, (d)->kH, (d)->kW, (d)->sH, (d)->sW, (d)->pH, (d)->pW
 
-int dlq_pack_conv_weights_s8(const int8_t* q, int OC, int IC, int kH, int kW, int C, int8_t* packed) {
-  if (!q || !packed || IC > C || packed_bytes(OC, C, kH, kW) == 0)
+size_t dlq_conv_packed_bytes(const dlq_conv_desc* d) { return d ? packed_bytes_for(DLQ_DESC_GEOM(d)) : 0; }
+
+int dlq_pack_conv_weights_s8(const dlq_conv_desc* d, const int8_t* q, int IC, int8_t* packed) {
+  if (!d || !q || !packed || IC <= 0 || IC > d->C || packed_bytes_for(DLQ_DESC_GEOM(d)) == 0)
     return fail(DLQ_ERR_ARG, "pack_conv_weights: unsupported shape (need C%64==0 or the 7x7 C=4 stem)");
-  pack_conv_weights(q, OC, IC, kH, kW, C, packed);
+  pack_conv_weights_for(DLQ_DESC_GEOM(d), q, IC, packed);
   return DLQ_OK;
 }
 
@@ -175,8 +198,10 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
   if (d->N < 0 || d->H <= 0 || d->W <= 0 || d->OC <= 0 || d->kH <= 0 || d->kW <= 0 || d->sH <= 0 ||
       d->sW <= 0 || d->pH < 0 || d->pW < 0)
     return fail(DLQ_ERR_ARG, "conv2d: bad shape");
-  if (packed_bytes(d->OC, d->C, d->kH, d->kW) == 0)
+  if (packed_bytes_for(DLQ_DESC_GEOM(d)) == 0)
     return fail(DLQ_ERR_ARG, "conv2d: unsupported C (need C%64==0, or C==4 with a 7x7 kernel)");
+  const bool wide = wide_layout(DLQ_DESC_GEOM(d));
+  if (wide && out_kind == DLQ_OUT_F32) return fail(DLQ_ERR_ARG, "conv2d: this shape supports int8 / int32 output");
   ConvArgs a{};
   a.x = x; a.w = w_packed; a.alpha = alpha; a.beta = beta; a.res = residual; a.y = y;
   a.s_res = res_scale;
@@ -200,7 +225,7 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
     return fail(DLQ_ERR_ARG, "conv2d: stem supports int8 (no residual) or int32 output");
   a.P = (int)P;
   if (a.P == 0) return DLQ_OK;
-  hipError_t e = launch_conv(a, (hipStream_t)stream);
+  hipError_t e = wide ? launch_conv3x3w(a, (hipStream_t)stream) : launch_conv(a, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d launch: ") + hipGetErrorString(e));
 }
 

@@ -56,4 +56,73 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
 
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// s_waitcnt vmcnt(N) expcnt(7) lgkmcnt(0) for a wave-uniform runtime N <= 63
+// (gfx9 encoding: vmcnt[3:0] in bits 3:0, vmcnt[5:4] in bits 15:14).  A
+// builtin per case so hipcc's waitcnt pass sees every wait.
+template <int N>
+__device__ __forceinline__ void wait_vm_const() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0070);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_sel(int n) {
+  if constexpr (N < 63) {
+    if (n == N) { wait_vm_const<N>(); return; }
+    wait_vm_sel<N + 1>(n);
+  } else {
+    wait_vm_const<63>();
+  }
+}
+__device__ __forceinline__ void wait_vm(int n) { wait_vm_sel<0>(n); }
+
+// The LDS input patch of a stride-1, pad-1 3x3 conv over a tile of
+// consecutive output pixels [p0, pend) (NHWC, pixel p = (n*H + oh)*W + ow):
+// the tile's rows plus a one-row halo above and below each image it touches,
+// no halo columns (taps left/right of the image read a zero region instead).
+// Slot order: image n0's rows oh0-1 .. (cnt0 slots), then each further image's
+// rows -1 .. H (H+2 slots each); a patch pixel index is slot*W + column.
+struct PatchTile {
+  int p0, pend, n0, oh0, cnt0, slots;
+};
+
+__device__ __forceinline__ PatchTile patch_tile(int p0, int pend, int W, int H) {
+  PatchTile t;
+  t.p0 = p0;
+  t.pend = pend;
+  const int R0 = p0 / W, R1 = (pend - 1) / W;
+  t.n0 = R0 / H;
+  t.oh0 = R0 - t.n0 * H;
+  const int n1 = R1 / H;
+  t.cnt0 = ((n1 == t.n0) ? (R1 - R0) : (H - 1 - t.oh0)) + 3;
+  t.slots = (n1 == t.n0) ? t.cnt0 : t.cnt0 + (n1 - t.n0 - 1) * (H + 2) + (R1 - n1 * H) + 3;
+  return t;
+}
+
+// slot -> (image, input row); the row may be -1 or H (halo outside the image).
+__device__ __forceinline__ void patch_slot(const PatchTile& t, int slot, int H, int& n, int& ih) {
+  if (slot < t.cnt0) {
+    n = t.n0;
+    ih = t.oh0 - 1 + slot;
+  } else {
+    const int s2 = slot - t.cnt0;
+    n = t.n0 + 1 + s2 / (H + 2);
+    ih = s2 % (H + 2) - 1;
+  }
+}
+
+// Output pixel p of the tile -> patch pixel index of its tap (kh=0, kw=1)
+// (= the pixel directly above), and the 9-bit mask of taps inside the image.
+__device__ __forceinline__ void patch_pixel(const PatchTile& t, int p, int W, int H, int& base, unsigned& mask) {
+  base = 0;
+  mask = 0;
+  if (p >= t.pend) return;
+  const int n = p / (H * W), r = p - n * (H * W), oh = r / W, ow = r - oh * W;
+  const int slot0 = (n == t.n0) ? oh - t.oh0 : t.cnt0 + (n - t.n0 - 1) * (H + 2) + oh;
+  base = slot0 * W + ow;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+      if ((unsigned)(oh + kh - 1) < (unsigned)H && (unsigned)(ow + kw - 1) < (unsigned)W) mask |= 1u << (kh * 3 + kw);
+}
+
 }  // namespace dlq

@@ -40,6 +40,11 @@ bool is_stem(int C, int kH, int kW);
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s);
 bool conv3x3s1_supported(const ConvArgs& a);
 hipError_t launch_conv3x3s1(const ConvArgs& a, hipStream_t s);
+// Wide stride-1 3x3 convs (conv3x3w.hip): own weight layout, selected by shape.
+bool conv3x3w_shape(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW);
+size_t conv3x3w_packed_bytes(int OC, int C);
+void conv3x3w_pack(const int8_t* q_oihw, int OC, int IC, int C, int8_t* out);
+hipError_t launch_conv3x3w(const ConvArgs& a, hipStream_t s);
 // Fused stem (stem.hip): quantise + conv1 7x7/s2 + BN/ReLU/requant + maxpool.
 size_t stem_packed_bytes();
 void pack_stem_weights(const int8_t* q_oihw, int8_t* out);
@@ -64,9 +69,15 @@ void quantize_weights(const float* w, int OC, int K, int8_t* q, float* scale);
 void fold_bn(float s_x, const float* s_w, const float* g, const float* b, const float* m,
              const float* v, float eps, float s_y, int OC, float* alpha, float* beta);
 float res_scale(float s_r, float s_y);
+// Generic / stem layouts (any shape the v1 kernel runs), and the
+// shape-selected image dlq_conv2d_nhwc_s8 expects (may be the wide layout).
 size_t packed_bytes(int OC, int C, int kH, int kW);
 void pack_conv_weights(const int8_t* q_oihw, int OC, int IC, int kH, int kW, int C,
                        int8_t* packed);
+bool wide_layout(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW);
+size_t packed_bytes_for(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW);
+void pack_conv_weights_for(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW,
+                           const int8_t* q_oihw, int IC, int8_t* packed);
 
 inline int out_dim(int in, int k, int s, int p) { return (in + 2 * p - k) / s + 1; }
 

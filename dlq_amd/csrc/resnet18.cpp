@@ -36,6 +36,7 @@ struct ConvLayer {
   std::string bn;       // state_dict BN prefix
   std::string in_site;  // scale site of the INPUT activation
   int IC = 0, OC = 0, k = 0, s = 1, p = 0, Cstore = 0;
+  int H = 0;            // input height = width
   int8_t* w = nullptr;  // packed weights (device)
   float* alpha = nullptr;
   float* beta = nullptr;
@@ -95,29 +96,31 @@ void build_topology(dlq_resnet18* m) {
   m->blocks.clear();
   ConvLayer st;
   st.site = "conv1"; st.wname = "conv1.weight"; st.bn = "bn1"; st.in_site = "input";
-  st.IC = 3; st.OC = 64; st.k = 7; st.s = 2; st.p = 3; st.Cstore = kStemC;
+  st.IC = 3; st.OC = 64; st.k = 7; st.s = 2; st.p = 3; st.Cstore = kStemC; st.H = 224;
   m->convs.push_back(st);
   m->stem = 0;
   std::string prev = "conv1";
+  int H = 56;
   for (int b = 0; b < 8; ++b) {
     const std::string n = kBlockNames[b];
     Block blk{n, kBlocks[b][0], kBlocks[b][1], kBlocks[b][2], kBlocks[b][3] != 0, 0, 0, -1};
     ConvLayer c1;
     c1.site = n + ".conv1"; c1.wname = n + ".conv1.weight"; c1.bn = n + ".bn1"; c1.in_site = prev;
-    c1.IC = blk.ic; c1.OC = blk.oc; c1.k = 3; c1.s = blk.stride; c1.p = 1; c1.Cstore = blk.ic;
+    c1.IC = blk.ic; c1.OC = blk.oc; c1.k = 3; c1.s = blk.stride; c1.p = 1; c1.Cstore = blk.ic; c1.H = H;
     blk.c1 = (int)m->convs.size();
     m->convs.push_back(c1);
     if (blk.down) {
       ConvLayer d;
       d.site = n + ".downsample"; d.wname = n + ".downsample.0.weight"; d.bn = n + ".downsample.1";
       d.in_site = prev;
-      d.IC = blk.ic; d.OC = blk.oc; d.k = 1; d.s = blk.stride; d.p = 0; d.Cstore = blk.ic;
+      d.IC = blk.ic; d.OC = blk.oc; d.k = 1; d.s = blk.stride; d.p = 0; d.Cstore = blk.ic; d.H = H;
       blk.ds = (int)m->convs.size();
       m->convs.push_back(d);
     }
     ConvLayer c2;
     c2.site = n + ".conv2"; c2.wname = n + ".conv2.weight"; c2.bn = n + ".bn2"; c2.in_site = c1.site;
-    c2.IC = blk.oc; c2.OC = blk.oc; c2.k = 3; c2.s = 1; c2.p = 1; c2.Cstore = blk.oc;
+    H /= blk.stride;
+    c2.IC = blk.oc; c2.OC = blk.oc; c2.k = 3; c2.s = 1; c2.p = 1; c2.Cstore = blk.oc; c2.H = H;
     blk.c2 = (int)m->convs.size();
     m->convs.push_back(c2);
     m->blocks.push_back(blk);
@@ -347,9 +350,9 @@ int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
     std::vector<int8_t> q((size_t)c.OC * K);
     std::vector<float> sw(c.OC);
     quantize_weights(w.data(), c.OC, K, q.data(), sw.data());
-    const size_t pb = packed_bytes(c.OC, c.Cstore, c.k, c.k);
+    const size_t pb = packed_bytes_for(c.Cstore, c.OC, c.H, c.H, c.k, c.k, c.s, c.s, c.p, c.p);
     std::vector<int8_t> packed(pb);
-    pack_conv_weights(q.data(), c.OC, c.IC, c.k, c.k, c.Cstore, packed.data());
+    pack_conv_weights_for(c.Cstore, c.OC, c.H, c.H, c.k, c.k, c.s, c.s, c.p, c.p, q.data(), c.IC, packed.data());
     std::vector<float> alpha(ocp, 0.f), beta(ocp, 0.f);
     fold_bn(m->scales.at(c.in_site), sw.data(), m->tensors.at(c.bn + ".weight").data(),
             m->tensors.at(c.bn + ".bias").data(), m->tensors.at(c.bn + ".running_mean").data(),

@@ -38,8 +38,8 @@ _SIGS = {
     "dlq_fold_bn": ([_f, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp], _i),
     "dlq_res_scale": ([_f, _f], _f),
     "dlq_conv_packed_oc": ([_i], _i),
-    "dlq_conv_packed_bytes": ([_i, _i, _i, _i], _sz),
-    "dlq_pack_conv_weights_s8": ([_vp, _i, _i, _i, _i, _i, _vp], _i),
+    "dlq_conv_packed_bytes": ([C.POINTER(ConvDesc)], _sz),
+    "dlq_pack_conv_weights_s8": ([C.POINTER(ConvDesc), _vp, _i, _vp], _i),
     "dlq_quantize_nchw_to_nhwc_s8": ([_vp, _i, _i, _i, _i, _i, _f, _vp, _vp], _i),
     "dlq_quantize_rows_s8": ([_vp, _i, _i, _i, _f, _vp, _vp], _i),
     "dlq_conv2d_nhwc_s8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp], _i),

@@ -54,15 +54,24 @@ def packed_oc(OC: int) -> int:
     return lib.dlq_conv_packed_oc(OC)
 
 
-def pack_conv_weights(q_oihw: np.ndarray, C_store: int) -> np.ndarray:
+def pack_conv_weights(q_oihw: np.ndarray, C_store: int, H: int, stride: int, pad: int) -> np.ndarray:
+    """Weight image of the conv over NHWC [*, H, H, C_store] with this kernel /
+    stride / pad -- the layout dlq_conv2d_nhwc_s8 expects for that descriptor."""
     q = np.ascontiguousarray(q_oihw, np.int8)
     OC, IC, kH, kW = q.shape
-    nb = lib.dlq_conv_packed_bytes(OC, C_store, kH, kW)
+    d = ConvDesc(1, H, H, C_store, OC, kH, kW, stride, stride, pad, pad)
+    nb = lib.dlq_conv_packed_bytes(C.byref(d))
     if nb == 0:
         raise ValueError(f"unsupported conv packing: C={C_store} k={kH}x{kW}")
     out = np.empty(nb, np.int8)
-    check(lib.dlq_pack_conv_weights_s8(ptr(q), OC, IC, kH, kW, C_store, ptr(out)), "pack_conv_weights")
+    check(lib.dlq_pack_conv_weights_s8(C.byref(d), ptr(q), IC, ptr(out)), "pack_conv_weights")
     return out
+
+
+def pack_linear_weights(q: np.ndarray, K: int | None = None) -> np.ndarray:
+    """Dense weights q[OC][IC] (IC <= K, K % 64 == 0) for dlq_linear_s8."""
+    OC, IC = q.shape
+    return pack_conv_weights(np.ascontiguousarray(q, np.int8).reshape(OC, IC, 1, 1), K or IC, 1, 1, 0)
 
 
 def pack_stem_weights(q_oihw: np.ndarray) -> np.ndarray:

@@ -73,30 +73,34 @@ float dlq_res_scale(float s_r, float s_y);
 
 /* Padded output-channel count the packed weights / alpha / beta must have. */
 int dlq_conv_packed_oc(int OC);
-/* Bytes of the packed weight image for a conv over NHWC input with C stored
- * channels.  Supported: C % 64 == 0 (any kH,kW), or the stem (C == 4,
- * kH == kW == 7).  Returns 0 for unsupported shapes. */
-size_t dlq_conv_packed_bytes(int OC, int C, int kH, int kW);
-/* Pack int8 OIHW weights q[OC][IC][kH][kW] (IC <= C; channels IC..C-1 and
- * padded rows are zero) into the kernels' image.  C % 64 == 0:
- *   [C/64][OCp/64][64 oc][kH*kW taps][4 x 16-byte chunks][16]
- * i.e. per (64-channel chunk, 64-output-channel tile) one contiguous block
- * that is copied verbatim into LDS; the 4 chunks of a 64-byte tap row are
- * stored at position chunk ^ ((oc%64 >> 2) & 3) (bank-conflict-free
- * ds_read_b128 of 16 consecutive output channels).
- * Stem (C == 4, 7x7): [OCp][8][8][4], taps padded to 8x8. */
-int dlq_pack_conv_weights_s8(const int8_t* q_oihw, int OC, int IC, int kH, int kW, int C,
-                             int8_t* packed);
-
-/* ------------------------------------------------------------------------ */
-/* Device operators (per-layer entry points; all asynchronous on `stream`)  */
-/* ------------------------------------------------------------------------ */
 
 typedef struct dlq_conv_desc {
   int N, H, W, C; /* input NHWC; C = stored channels (4 for the RGB stem)     */
   int OC;         /* output channels                                          */
   int kH, kW, sH, sW, pH, pW;
 } dlq_conv_desc;
+
+/* Bytes of the packed weight image for the conv `d` (N is ignored).  The
+ * image is specific to the descriptor, like a cuDNN filter transform: the
+ * kernel that dlq_conv2d_nhwc_s8 selects for `d` reads exactly this layout.
+ * Supported: C % 64 == 0 (any kH, kW), the stem (C == 4, 7x7), and C % 32 ==
+ * 0 for the wide stride-1 3x3 convs.  Returns 0 for unsupported shapes.
+ * Layouts (q = OIHW int8):
+ *  - wide stride-1 3x3 (C == OC in {128 @28x28, 256 @14x14, 512 @7x7}, s1 p1):
+ *      [OCp/128][C/32][128 oc][9 taps x 32 channels + 16 zero bytes]
+ *    one contiguous 38,912-byte block per (128-oc tile, 32-channel slice),
+ *    copied verbatim into LDS (row pitch 304 B: conflict-free ds_read_b128);
+ *  - stem (C == 4, 7x7): [OCp][8][8][4], taps padded to 8x8;
+ *  - otherwise (C % 64 == 0): [C/64][OCp/64][64 oc][kH*kW taps][4 x 16 B]
+ *    with the 4 chunks of a 64-byte tap row stored at chunk ^ ((oc%64>>2)&3). */
+size_t dlq_conv_packed_bytes(const dlq_conv_desc* d);
+/* Pack q_oihw[OC][IC][kH][kW] (IC <= C; channels IC..C-1 and padded output
+ * rows are zero) into the image dlq_conv_packed_bytes(d) describes. */
+int dlq_pack_conv_weights_s8(const dlq_conv_desc* d, const int8_t* q_oihw, int IC, int8_t* packed);
+
+/* ------------------------------------------------------------------------ */
+/* Device operators (per-layer entry points; all asynchronous on `stream`)  */
+/* ------------------------------------------------------------------------ */
 
 /* Input quantisation (new; the reference feeds fp32 straight to im2col,
  * RK/runtime/infer_e2e.cu:255-256): fp32 NCHW x[N][C][H][W] ->
@@ -136,8 +140,9 @@ int dlq_pack_stem_weights_s8(const int8_t* q_oihw, int8_t* packed);
 int dlq_stem_fused_s8(const float* x, int N, const int8_t* w_stem, const float* alpha, const float* beta,
                       float inv_s, int8_t* y, void* stream);
 
-/* Dense layer on int8 rows: y[N][OC] from x[N][K] (K % 64 == 0) and packed
- * weights [OCp][K]; same epilogue kinds.  Replaces fc_forward
+/* Dense layer on int8 rows: y[N][OC] from x[N][K] (K % 64 == 0) and weights
+ * packed as the 1x1 conv {H = W = 1, C = K, OC} (dlq_pack_conv_weights_s8);
+ * same epilogue kinds.  Replaces fc_forward
  * (RK/runtime/infer_e2e.cu:206-219: sgemm_tiled M=1000,N=1,K=512 + host bias)
  * and the MNIST forward GEMMs (CUDA/MNIST_on_GPU/v4.cu:255-302
  * matmul_a_b_kernel + bias_forward_kernel + relu_forward_kernel;

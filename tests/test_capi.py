@@ -62,7 +62,7 @@ def test_pack_layout():
     q = rng.integers(-127, 128, size=(100, 128, 3, 3), dtype=np.int8)
     ocp = ops.packed_oc(100)
     # [C/64][OCp/64][64 oc][9 taps][4 chunks of 16, stored at chunk ^ ((oc%64>>2)&3)]
-    p = ops.pack_conv_weights(q, 128).reshape(2, ocp // 64, 64, 9, 4, 16)
+    p = ops.pack_conv_weights(q, 128, 56, 1, 1).reshape(2, ocp // 64, 64, 9, 4, 16)
     oc = np.arange(ocp).reshape(ocp // 64, 64)
     perm = (np.arange(4)[None, :] ^ ((np.arange(64)[:, None] >> 2) & 3))  # [ol][logical chunk] -> stored pos
     logical = np.empty_like(p)
@@ -73,9 +73,24 @@ def test_pack_layout():
     assert np.array_equal(dense[:100], np.transpose(q, (0, 2, 3, 1)))
     assert not dense[100:].any() and oc.size == ocp
     qs = rng.integers(-127, 128, size=(64, 3, 7, 7), dtype=np.int8)
-    ps = ops.pack_conv_weights(qs, 4).reshape(64, 8, 8, 4)
+    ps = ops.pack_conv_weights(qs, 4, 224, 2, 3).reshape(64, 8, 8, 4)
     assert np.array_equal(ps[:, :7, :7, :3], np.transpose(qs, (0, 2, 3, 1)))
     assert not ps[:, 7].any() and not ps[:, :, 7].any() and not ps[..., 3].any()
+
+
+@pytest.mark.parametrize("C,H", [(128, 28), (256, 14), (512, 7)])
+def test_pack_layout_wide_s1(C, H):
+    """Wide stride-1 3x3 convs: [OC/128][C/32][128 oc][9 taps x 32 ch + 16 zero]."""
+    from dlq_amd import ops
+    rng = np.random.default_rng(C)
+    q = rng.integers(-127, 128, size=(C, C, 3, 3), dtype=np.int8)
+    p = ops.pack_conv_weights(q, C, H, 1, 1).reshape(C // 128, C // 32, 128, 304)
+    assert not p[..., 288:].any()
+    taps = p[..., :288].reshape(C // 128, C // 32, 128, 9, 32)      # [ot][j][ol][tap][cc]
+    dense = taps.transpose(0, 2, 3, 1, 4).reshape(C, 3, 3, C)        # [oc][kh][kw][c]
+    assert np.array_equal(dense, np.transpose(q, (0, 2, 3, 1)))
+    # the same weights for a stride-2 conv or another resolution keep the generic layout
+    assert ops.pack_conv_weights(q, C, 2 * H, 1, 1).size == C * 9 * C
 
 
 def test_errors_are_returned_not_exited():
@@ -83,7 +98,7 @@ def test_errors_are_returned_not_exited():
     d = ConvDesc(1, 8, 8, 3, 8, 3, 3, 1, 1, 1, 1)  # C=3 with a 3x3 kernel: unsupported
     rc = lib.dlq_conv2d_nhwc_s8(C.byref(d), 1, 1, 1, 1, None, 0.0, 1, 0, 1, None)
     assert rc == 1 and b"unsupported" in lib.dlq_last_error()
-    assert lib.dlq_conv_packed_bytes(8, 3, 3, 3) == 0
+    assert lib.dlq_conv_packed_bytes(C.byref(d)) == 0
     h = C.c_void_p()
     assert lib.dlq_resnet18_create(C.byref(h)) == 0
     try:

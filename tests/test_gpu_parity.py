@@ -36,14 +36,14 @@ def _cuda(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
-def _gpu_conv_inputs(x_nchw, wq, k):
+def _gpu_conv_inputs(x_nchw, wq, s, p):
     from dlq_amd import ops
     IC = wq.shape[1]
     c_store = 4 if IC == 3 else IC
     xh = nchw_to_nhwc(x_nchw)
     if c_store != IC:
         xh = np.concatenate([xh, np.zeros(xh.shape[:3] + (c_store - IC,), np.int8)], axis=3)
-    packed = ops.pack_conv_weights(wq, c_store)
+    packed = ops.pack_conv_weights(wq, c_store, x_nchw.shape[2], s, p)
     return _cuda(xh), _cuda(packed)
 
 
@@ -58,15 +58,15 @@ def test_conv_int32_accumulators_bitexact(gpu, shape):
     w, _ = rand_conv(rng, OC, IC, k)
     wq, _ = O.quantize_weights_s8(w)
     ref = O.conv_s8_acc(x, wq, s, p)
-    xd, wd = _gpu_conv_inputs(x, wq, k)
+    xd, wd = _gpu_conv_inputs(x, wq, s, p)
     acc = ops.conv2d_nhwc_s8(xd, wd, OC, k, s, p, out_kind=DLQ_OUT_S32)
     got = nhwc_to_nchw(acc.cpu().numpy())
     assert got.shape == ref.shape
     assert np.array_equal(got, ref), f"{name}: {np.count_nonzero(got != ref)} int32 mismatches"
 
 
-@pytest.mark.parametrize("shape", [CONV_SHAPES[i] for i in (0, 1, 2, 4, 6, 9)],
-                         ids=[CONV_SHAPES[i][0] for i in (0, 1, 2, 4, 6, 9)])
+@pytest.mark.parametrize("shape", [CONV_SHAPES[i] for i in (0, 1, 2, 3, 4, 6, 9)],
+                         ids=[CONV_SHAPES[i][0] for i in (0, 1, 2, 3, 4, 6, 9)])
 @pytest.mark.parametrize("residual", [False, True])
 def test_conv_fused_epilogue_bitexact(gpu, shape, residual):
     from dlq_amd import ops
@@ -85,7 +85,7 @@ def test_conv_fused_epilogue_bitexact(gpu, shape, residual):
     res = rand_s8(rng, acc.shape) if residual else None
     relu = (k != 1)  # downsample convs have no ReLU (infer_e2e.cu:187-196)
     ref = O.epilogue_s8(acc, alpha, beta, res, r_s, relu)
-    xd, wd = _gpu_conv_inputs(x, wq, k)
+    xd, wd = _gpu_conv_inputs(x, wq, s, p)
     ocp = ops.packed_oc(OC)
     a_alpha, a_beta = ops.fold_bn(s_x, sw, *bn, s_y)
     assert np.array_equal(a_alpha, alpha) and np.array_equal(a_beta, beta)  # host prep == oracle
@@ -116,6 +116,29 @@ def test_stem_fused_bitexact(gpu, N):
     assert np.array_equal(got, ref), f"{np.count_nonzero(got != ref)} int8 mismatches"
 
 
+@pytest.mark.parametrize("C,H,N", [(128, 28, 90), (256, 14, 180), (512, 7, 360)])
+def test_wide_conv_many_items_per_workgroup(gpu, C, H, N):
+    """Batches large enough that every workgroup of the wide stride-1 kernel
+    walks several items (ring wrap-around, item hand-over): sampled images
+    against the oracle, each computed alone (a conv is per image)."""
+    from dlq_amd import ops
+    rng = np.random.default_rng(C + N)
+    x = rand_s8(rng, (N, C, H, H))
+    w, bn = rand_conv(rng, C, C, 3)
+    wq, sw = O.quantize_weights_s8(w)
+    s_x, s_y, s_r = 0.029, 0.051, 0.044
+    alpha, beta = O.fold_bn(s_x, sw, bn, s_y)
+    r_s = O.res_scale(s_r, s_y)
+    res = rand_s8(rng, (N, C, H, H))
+    xd, wd = _gpu_conv_inputs(x, wq, 1, 1)
+    y = ops.conv2d_nhwc_s8(xd, wd, C, 3, 1, 1, _cuda(alpha), _cuda(beta), residual=_cuda(nchw_to_nhwc(res)),
+                           res_scale=r_s, relu=True)
+    got = nhwc_to_nchw(y.cpu().numpy())
+    for i in (0, 1, N // 2, N - 2, N - 1):
+        ref = O.epilogue_s8(O.conv_s8_acc(x[i:i + 1], wq, 1, 1), alpha, beta, res[i:i + 1], r_s, True)
+        assert np.array_equal(got[i:i + 1], ref), f"image {i}: {np.count_nonzero(got[i:i + 1] != ref)} mismatches"
+
+
 def test_fc_logits_bitexact(gpu):
     from dlq_amd import ops
     from dlq_amd.lib import DLQ_OUT_F32, DLQ_OUT_S32
@@ -128,7 +151,7 @@ def test_fc_logits_bitexact(gpu):
         x = rand_s8(rng, (N, 512), lo=0)
         alpha = O.fc_alpha(0.02, sw)
         ref, racc = O.fc_s8(x, wq, alpha, bias)
-        packed = _cuda(ops.pack_conv_weights(wq.reshape(1000, 512, 1, 1), 512))
+        packed = _cuda(ops.pack_linear_weights(wq))
         ocp = ops.packed_oc(1000)
         acc = ops.linear_s8(_cuda(x), packed, 1000, out_kind=DLQ_OUT_S32)
         assert np.array_equal(acc.cpu().numpy(), racc)
