@@ -231,9 +231,9 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
 
 size_t dlq_stem_packed_bytes(void) { return stem_packed_bytes(); }
 
-int dlq_pack_stem_weights_s8(const int8_t* q_oihw, int8_t* packed) {
-  if (!q_oihw || !packed) return fail(DLQ_ERR_ARG, "pack_stem_weights: null");
-  pack_stem_weights(q_oihw, packed);
+int dlq_pack_stem_weights_s8(const int8_t* q_oihw, const float* alpha, int8_t* packed, float* alpha_packed) {
+  if (!q_oihw || !alpha || !packed || !alpha_packed) return fail(DLQ_ERR_ARG, "pack_stem_weights: null");
+  pack_stem_weights(q_oihw, alpha, packed, alpha_packed);
   return DLQ_OK;
 }
 

@@ -47,7 +47,7 @@ void conv3x3w_pack(const int8_t* q_oihw, int OC, int IC, int C, int8_t* out);
 hipError_t launch_conv3x3w(const ConvArgs& a, hipStream_t s);
 // Fused stem (stem.hip): quantise + conv1 7x7/s2 + BN/ReLU/requant + maxpool.
 size_t stem_packed_bytes();
-void pack_stem_weights(const int8_t* q_oihw, int8_t* out);
+void pack_stem_weights(const int8_t* q_oihw, const float* alpha, int8_t* out, float* alpha_abs);
 hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float* alpha, const float* beta,
                              float inv_s, int8_t* y, hipStream_t s);
 hipError_t launch_quantize_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cout,

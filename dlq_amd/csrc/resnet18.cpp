@@ -57,7 +57,8 @@ struct dlq_resnet18 {
   std::vector<ConvLayer> convs;
   std::vector<Block> blocks;
   int stem = -1;
-  int8_t* stem_w = nullptr;  // fused-stem weight image (dlq_pack_stem_weights_s8)
+  int8_t* stem_w = nullptr;       // fused-stem weight image (dlq_pack_stem_weights_s8)
+  float* stem_alpha = nullptr;    // |alpha| of conv1 for the fused stem
   // FC
   int8_t* fc_w = nullptr;
   float* fc_alpha = nullptr;
@@ -169,6 +170,7 @@ void free_all(dlq_resnet18* m) {
   for (auto& c : m->convs) { c.w = nullptr; c.alpha = nullptr; c.beta = nullptr; }
   m->fc_w = nullptr; m->fc_alpha = m->fc_beta = nullptr;
   m->xq = m->c1 = m->gq = m->stem_w = nullptr;
+  m->stem_alpha = nullptr;
   for (auto& b : m->buf) b = nullptr;
   m->keepbuf.clear();
   m->prepared = false;
@@ -368,9 +370,11 @@ int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
       return hip_fail(e, "weight upload");
     if (&c == &m->convs[m->stem]) {  // the fused stem's space-to-depth weight image
       std::vector<int8_t> sp(stem_packed_bytes());
-      pack_stem_weights(q.data(), sp.data());
-      if ((rc = dev_alloc(m, &m->stem_w, sp.size()))) return rc;
-      if ((e = hipMemcpy(m->stem_w, sp.data(), sp.size(), hipMemcpyHostToDevice)) != hipSuccess)
+      std::vector<float> sa(64);
+      pack_stem_weights(q.data(), alpha.data(), sp.data(), sa.data());
+      if ((rc = dev_alloc(m, &m->stem_w, sp.size())) || (rc = dev_alloc(m, &m->stem_alpha, 64 * 4))) return rc;
+      if ((e = hipMemcpy(m->stem_w, sp.data(), sp.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+          (e = hipMemcpy(m->stem_alpha, sa.data(), 64 * 4, hipMemcpyHostToDevice)) != hipSuccess)
         return hip_fail(e, "stem weight upload");
     }
   }
@@ -440,7 +444,7 @@ int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, 
     // 0+1) fused stem: quantise + conv 7x7/s2 + BN + ReLU + maxpool 3x3/s2
     //      (infer_e2e.cu:255-293) in one launch
     if ((rc = mark(m, s))) return rc;
-    rc = dlq_stem_fused_s8(x, B, m->stem_w, st.alpha, st.beta, inv_scale(m->scales.at("input")), cur, stream);
+    rc = dlq_stem_fused_s8(x, B, m->stem_w, m->stem_alpha, st.beta, inv_scale(m->scales.at("input")), cur, stream);
     if (rc) return rc;
     if ((rc = mark(m, s))) return rc;
   } else {

@@ -1,205 +1,235 @@
 // stem.hip -- fused ResNet-18 stem: input quantisation + conv1 7x7/s2/p3 (+BN,
-// ReLU, requant) + maxpool 3x3/s2/p1 in one persistent kernel.
+// ReLU, requant) + maxpool 3x3/s2/p1 in one kernel.
 //
 // Replaces (RK = CUDA/resnet18-kernel-lab/cpp/fp32): the input upload
 // (RK/runtime/infer_e2e.cu:255-256), conv2d_nchw_im2col_gemm for conv1
 // (:259-270, im2col_nchw + sgemm_tiled), bn_launch + relu_forward (:272-280)
-// and maxpool2d_3x3_s2p1_nchw (:282-293).  The conv1 output (64 x 112 x 112
-// per image, 4x the pooled size) never reaches HBM.
+// and maxpool2d_3x3_s2p1_nchw (:282-293).  The 112x112x64 conv1 output never
+// leaves the register file.
 //
-// Space-to-depth: the 224x224x3 fp32 image is read as a 112x112 grid of
-// 16-byte "super-pixels" [dy][dx][c] (2x2 pixels x RGB+0), quantised on the
-// fly.  The 7x7/s2 conv becomes a 4x4/s1 conv over super-pixels whose taps
-// cover input rows/cols 2*o-4 .. 2*o+3 (kh = 2*ky+dy-1; kh = -1 carries a zero
-// weight), i.e. K = 16 taps x 16 B = 256 = 8 steps of v_mfma_i32_32x32x32_i8,
-// and every B fragment is one 16-byte-aligned ds_read_b128 of consecutive
-// super-pixels (conflict-free).
+// Input: the fp32 rows stream through an LDS-DMA ring and are quantised into a
+// ring of "super rows": 2x2 pixels x (RGB, 0) = 16-byte super-pixels, so the
+// 7x7/s2 conv is a 4x4/s1 conv over super-pixels (kh = 2*ky+dy-1; kh = -1
+// carries a zero weight) with K = 16 super taps x 16 B = 8 steps of
+// v_mfma_i32_32x32x32_i8, every A fragment one ds_read_b128.
 //
-// Work item = a band of 4 pooled rows (x 56) of one image = 9 conv rows x 112
-// (the 9th conv row is the pool halo shared with the band above, recomputed).
-// One 512-thread workgroup per CU walks bands; the next band's fp32 input is
-// loaded into registers while the current band's MFMAs run.
+// MFMA orientation D[px][oc]: A = 32 conv pixels of one conv row, B = 32 output
+// channels held in registers for the whole kernel.  A-row i is conv column
+// c0 + pi(i) with pi chosen so that D register r of lane half h holds column
+// c0 + 16h + r: each lane owns 16 consecutive columns of ONE channel, and the
+// 3x3/s2 max pool runs on the int32 accumulators in registers (v_max3_i32).
+// Pooling before the epilogue is exact because the epilogue y = fma(acc, a, b)
+// -> clamp -> rne is monotone non-decreasing in acc once a >= 0; channels with
+// a < 0 have their weights (and a) negated at packing time
+// (dlq_pack_stem_weights_s8).  Only the pooled values (1/4 of the conv
+// outputs) are requantised.
+//
+// Work item = (image, band of pooled rows).  8 waves = 2 channel tiles x 4
+// column quarters; quarter q computes conv columns 28q-1 .. 28q+30 (32, of
+// which 29 are used) and produces pooled columns 14q .. 14q+13.  A step
+// computes conv rows 2p, 2p+1 and emits pooled row p.
 #include "device_common.h"
 
 namespace dlq {
 namespace {
 
-constexpr int PR = 4;                 // pooled rows per band
-constexpr int CR = 2 * PR + 1;        // conv rows per band
-constexpr int SR = CR + 3;            // super-pixel rows per band
-constexpr int SC = 115;               // super-pixel cols (-2 .. 112)
-constexpr int CPX = CR * 112;         // conv pixels per band (1008)
-constexpr int NW = 8;                 // waves
-constexpr int NTH = NW * 64;
-constexpr int FN = 4;                 // 32-px MFMA tiles per wave (8 waves x 4 x 32 = 1024 >= 1008)
-constexpr int WPITCH = 272;           // LDS row pitch of the weight image (256 + 16: conflict-free)
-constexpr int UNITS = SR * SC;        // super-pixels per band (1380)
-constexpr int UPT = (UNITS + NTH - 1) / NTH;  // per thread (3)
-
-constexpr int OFF_P = 0;                          // patch: SR x SC x 16 B
-constexpr int OFF_W = OFF_P + SR * SC * 16;       // weights: 64 x 272 B
-constexpr int OFF_C = OFF_W + 64 * WPITCH;        // conv tile: CR x 112 x 64 B (chunk-swizzled)
-constexpr int OFF_AB = OFF_C + CPX * 64;          // alpha, beta: 64 + 64 floats
-constexpr int LDS_TOTAL = OFF_AB + 512;
-static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
+constexpr int SNW = 8;                   // waves
+constexpr int SLA = 6;                   // raw-row pairs in flight ahead of the converter (>= 3)
+constexpr int RAW_SLOTS = SLA + 1;       // raw ring: pairs of super rows (12 x 1 KiB input rows)
+constexpr int RAW_SLOT_BYTES = 12 * 1024;
+constexpr int PATCH_SLOTS = 8;           // super-row ring
+constexpr int PATCH_ROW = 128 * 16;      // super cols -4 .. 123
+constexpr int OFF_RAW = 0;
+constexpr int OFF_PATCH = OFF_RAW + RAW_SLOTS * RAW_SLOT_BYTES;
+constexpr int OFF_STAGE = OFF_PATCH + PATCH_SLOTS * PATCH_ROW;  // per wave 16 x 32 B output staging
+constexpr int LDS_STEM = OFF_STAGE + SNW * 512;
+static_assert(LDS_STEM <= 160 * 1024, "LDS budget");
+constexpr int kIntMin = (int)0x80000000;
 
 struct StemArgs {
   const float* x;      // [N][3][224][224]
-  const int8_t* w;     // [64][256]  (oc, ky, kx, dy, dx, c)
-  const float* alpha;  // [64] output-grid units
+  const int8_t* w;     // [64][16 super taps][16 B] (dlq_pack_stem_weights_s8)
+  const float* alpha;  // [64] |alpha| (packed), output-grid units
   const float* beta;   // [64]
   int8_t* y;           // [N][56][56][64]
   float inv_s;         // 1 / input scale
-  int N;
-  int dbg;             // ablation bits (timing builds only): 1 MFMA, 2 input loads, 4 epilogue+pool, 8 patch store
+  int N, nb, R;        // batch, bands per image, pooled rows per band
 };
 
-__global__ __launch_bounds__(NTH, 1) void stem_fused_kernel(StemArgs a) {
-  __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
+__device__ __forceinline__ void swap32s(unsigned& x, unsigned& y) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+  x = r[0];
+  y = r[1];
+}
+
+__device__ __forceinline__ int max3i(int a, int b, int c) {
+  return __builtin_elementwise_max(__builtin_elementwise_max(a, b), c);
+}
+
+// One LDS-DMA piece from asm: the builtin's LDS memory operand makes hipcc's
+// waitcnt pass drain every later ds_read with lgkmcnt(0) (see conv3x3w.hip).
+// Completion is covered by the explicit vmcnt counts + barrier below.
+__device__ __forceinline__ void glds16_stem(const void* gsrc, unsigned lds_addr) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "{m0}"(m0) : "memory");
+}
+
+__global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
+  __shared__ __attribute__((aligned(16))) int8_t lds[LDS_STEM];
+  const unsigned lds32 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) int8_t*)lds;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 31, lh = lane >> 5;
-  const int nbands = a.N * (56 / PR);
+  const int ot = wave & 1, q = wave >> 1;  // channel tile, column quarter
+  const int D = wave < 4 ? 2 : 1;          // raw DMA pieces per pair issued by this wave
+  const int nitems = a.N * a.nb;
 
-  // weights (once per workgroup) + epilogue constants
-  for (int i = tid; i < 64 * 16; i += NTH) {
-    const int oc = i >> 4, t = i & 15;
-    *(v4i*)(lds + OFF_W + oc * WPITCH + t * 16) = *(const v4i*)(a.w + oc * 256 + t * 16);
+  // B fragments (weights) for all 8 k-steps, and the channel's epilogue constants.
+  v4i wreg[8];
+  {
+    const int8_t* wp = a.w + (ot * 32 + lr) * 256 + lh * 16;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) wreg[kk] = *(const v4i*)(wp + kk * 32);
   }
-  if (tid < 64) {
-    ((float*)(lds + OFF_AB))[tid] = a.alpha[tid];
-    ((float*)(lds + OFF_AB))[64 + tid] = a.beta[tid];
-  }
+  const float al = a.alpha[ot * 32 + lr], be = a.beta[ot * 32 + lr];
+  wait_vm_const<0>();  // before any LDS-DMA is counted
+  // A-row permutation: lane row i -> conv column offset pi(i) (D reg r of half h = column 16h + r)
+  const int pi = ((lr >> 3) << 2) + (lr & 3) + 16 * ((lr >> 2) & 1);
+  const int a_unit = 28 * q + 1 + pi;  // super-col unit of tap kx = 0 (unit = super col + 4)
+  int8_t* stg = lds + OFF_STAGE + wave * 512;
 
-  // Prefetch registers: UPT super-pixels x (3 channels x 2 rows) float2.
-  float2 pf[UPT][6];
-  auto load_band = [&](int band) {
-    const int n = band / (56 / PR), py0 = (band % (56 / PR)) * PR;
-    const int sy0 = 2 * py0 - 1 - 2;  // super row of patch row 0 (conv row 2*py0-1, tap ky=0)
+  for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+    const int n = item / a.nb, band = item - n * a.nb;
+    const int py0 = band * a.R, py1 = min(56, py0 + a.R);
+    if (py0 >= py1) continue;
+    const int sr0 = 2 * py0 - 3;  // first super row (pair k = super rows sr0+2k, sr0+2k+1)
     const float* img = a.x + (size_t)n * 3 * 224 * 224;
-#pragma unroll
-    for (int k = 0; k < UPT; ++k) {
-      const int u = tid + k * NTH;
-      const int sr = u / SC, sc = u - sr * SC;
-      const int sy = sy0 + sr, sx = sc - 2;
-      const bool ok = u < UNITS && (unsigned)sy < 112u && (unsigned)sx < 112u;
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-#pragma unroll
-        for (int dy = 0; dy < 2; ++dy)
-          pf[k][c * 2 + dy] = ok && !(a.dbg & 2) ? *(const float2*)(img + ((size_t)c * 224 + 2 * sy + dy) * 224 + 2 * sx)
-                                 : make_float2(0.f, 0.f);
-    }
-  };
-  auto store_patch = [&]() {
-#pragma unroll
-    for (int k = 0; k < UPT; ++k) {
-      const int u = tid + k * NTH;
-      if (u >= UNITS) continue;
-      unsigned w4[4];  // bytes [dy][dx][c], c = 3 is zero
-#pragma unroll
-      for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 2; ++dx) {
-          unsigned v = 0;
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const float f = dx ? pf[k][c * 2 + dy].y : pf[k][c * 2 + dy].x;
-            v |= ((unsigned)sat_rne(f * a.inv_s) & 0xffu) << (8 * c);
-          }
-          w4[dy * 2 + dx] = v;
-        }
-      *(v4i*)(lds + OFF_P + u * 16) = v4i{(int)w4[0], (int)w4[1], (int)w4[2], (int)w4[3]};
-    }
-  };
 
-  // lane-constant A offsets
-  int a_off[2];
+    // Raw pair k -> ring slot k % RAW_SLOTS: 12 input rows (2 super rows x 3
+    // channels x 2 pixel rows), 896 B each in a 1 KiB piece.  Waves 0-3 issue
+    // two pieces per pair, waves 4-7 one.
+    auto issue_pair = [&](int k) {
+      const unsigned slot = lds32 + OFF_RAW + (k % RAW_SLOTS) * RAW_SLOT_BYTES;
 #pragma unroll
-  for (int fm = 0; fm < 2; ++fm) a_off[fm] = OFF_W + (fm * 32 + lr) * WPITCH + lh * 16;
-  // lane pixel -> patch offset of super tap (0,0)
-  int b_off[FN];
-#pragma unroll
-  for (int fn = 0; fn < FN; ++fn) {
-    int px = (wave * FN + fn) * 32 + lr;
-    px = px < CPX ? px : CPX - 1;
-    const int r = px / 112, ox = px - r * 112;
-    b_off[fn] = OFF_P + (r * SC + ox) * 16;
-  }
-
-  int band = blockIdx.x;
-  if (band < nbands) load_band(band);
-  for (; band < nbands; band += gridDim.x) {
-    __syncthreads();  // previous band's conv tile fully pooled, patch free
-    if (!(a.dbg & 8)) store_patch();
-    __syncthreads();
-    if (band + (int)gridDim.x < nbands) load_band(band + gridDim.x);  // in flight during the MFMAs
-
-    v16i acc[2][FN];
-#pragma unroll
-    for (int fm = 0; fm < 2; ++fm)
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = v16i{0};
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      if (a.dbg & 1) break;
-      const int t = 2 * kk + lh, ky = t >> 2, kx = t & 3;  // this lane's super tap
-      v4i af[2], bf[FN];
-#pragma unroll
-      for (int fm = 0; fm < 2; ++fm) af[fm] = *(const v4i*)(lds + a_off[fm] + kk * 32);
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) bf[fn] = *(const v4i*)(lds + b_off[fn] + (ky * SC + kx) * 16);
-#pragma unroll
-      for (int fm = 0; fm < 2; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
-    }
-
-    if (a.dbg & 4) {  // keep the accumulators live
-      if (acc[0][0][0] == 0x7fffffff && acc[1][FN - 1][15] == 0x7fffffff) a.y[0] = 1;
-      continue;
-    }
-    // epilogue: BN*requant + ReLU -> int8 conv tile [r][ox][64] (chunk-swizzled by pixel)
-    const float* s_al = (const float*)(lds + OFF_AB);
-#pragma unroll
-    for (int fn = 0; fn < FN; ++fn) {
-      const int px = (wave * FN + fn) * 32 + lr;
-#pragma unroll
-      for (int fm = 0; fm < 2; ++fm)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int ol = fm * 32 + 8 * g + 4 * lh;
-          float v[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            v[j] = __builtin_fmaf((float)acc[fm][fn][4 * g + j], s_al[ol + j], s_al[64 + ol + j]);
-          const unsigned q = quant4(v[0], v[1], v[2], v[3], 0.f);
-          if (px < CPX)
-            *(unsigned*)(lds + OFF_C + px * 64 + (((ol >> 4) ^ ((px >> 2) & 3)) << 4) + ((ol >> 2) & 3) * 4) = q;
-        }
-    }
-    __syncthreads();
-
-    // 3x3/s2/p1 max pool of the band -> pooled int8 NHWC, 16 channels per lane
-    const int n = band / (56 / PR), py0 = (band % (56 / PR)) * PR;
-    for (int u = tid; u < PR * 56 * 4; u += NTH) {
-      const int ch = u & 3, pp = u >> 2, ppy = pp / 56, ppx = pp - ppy * 56;
-      v16c m = (v16c)(signed char)-128;
-#pragma unroll
-      for (int dr = 0; dr < 3; ++dr) {
-        const int r = 2 * ppy + dr;
-        if (py0 == 0 && r == 0) continue;  // conv row -1: pool padding
-#pragma unroll
-        for (int dc = 0; dc < 3; ++dc) {
-          const int ox = 2 * ppx - 1 + dc;
-          if (ox < 0) continue;
-          const int px = r * 112 + ox;
-          const v16c v = *(const v16c*)(lds + OFF_C + px * 64 + ((ch ^ ((px >> 2) & 3)) << 4));
-          m = __builtin_elementwise_max(m, v);
+      for (int d = 0; d < 2; ++d) {
+        const int j = wave + 8 * d;
+        if (j < 12) {
+          const int sr = sr0 + 2 * k + j / 6, c = (j % 6) >> 1, dy = j & 1;
+          const bool ok = (unsigned)sr < 112u;
+          const int l = lane < 56 ? lane : 55;
+          const float* src = ok ? img + ((size_t)c * 224 + 2 * sr + dy) * 224 + l * 4 : a.x;
+          glds16_stem(src, slot + j * 1024);
         }
       }
-      *(v16c*)(a.y + (((size_t)n * 56 + py0 + ppy) * 56 + ppx) * 64 + ch * 16) = m;
+    };
+    // Quantise raw pair k into two super rows of the patch ring: waves 0-1
+    // the first row, waves 2-3 the second; 128 units = super cols -4..123.
+    auto convert_pair = [&](int k) {
+      if (wave >= 4) return;
+      const int h = wave >> 1, unit = tid & 127, sc = unit - 4;
+      const int sr = sr0 + 2 * k + h;
+      v4i out = {0, 0, 0, 0};
+      if ((unsigned)sr < 112u && (unsigned)sc < 112u) {
+        const int8_t* raw = lds + OFF_RAW + (k % RAW_SLOTS) * RAW_SLOT_BYTES + h * 6 * 1024 + sc * 8;
+        unsigned u[3][2][2];  // [c][dy][dx]: clamp(x/s) + 1.5*2^23 -> rne'd int8 in the low byte
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+          for (int dy = 0; dy < 2; ++dy) {
+            const int2 f = *(const int2*)(raw + (c * 2 + dy) * 1024);  // dx = 0, 1 (read as ints)
+            u[c][dy][0] = __float_as_uint(
+                __builtin_amdgcn_fmed3f(__int_as_float(f.x) * a.inv_s, -127.f, 127.f) + 12582912.0f);
+            u[c][dy][1] = __float_as_uint(
+                __builtin_amdgcn_fmed3f(__int_as_float(f.y) * a.inv_s, -127.f, 127.f) + 12582912.0f);
+          }
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 2; ++dx) {  // bytes (c0, c1, c2, 0)
+            const unsigned t = __builtin_amdgcn_perm(u[1][dy][dx], u[0][dy][dx], 0x0c0c0400u);
+            out[dy * 2 + dx] = (int)__builtin_amdgcn_perm(u[2][dy][dx], t, 0x0c040100u);
+          }
+      }
+      *(v4i*)(lds + OFF_PATCH + (sr & (PATCH_SLOTS - 1)) * PATCH_ROW + unit * 16) = out;
+    };
+    // One conv row (global row oy): the wave's 32 px x 32 oc tile, 8 k-steps.
+    auto conv_row = [&](int oy) {
+      v4i af[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const int sr = oy - 2 + (kk >> 1);  // ky = kk/2, kx = 2*(kk&1) + lh
+        af[kk] = *(const v4i*)(lds + OFF_PATCH + (sr & (PATCH_SLOTS - 1)) * PATCH_ROW +
+                               (a_unit + 2 * (kk & 1) + lh) * 16);
+      }
+      v16i acc = v16i{0};
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[kk], wreg[kk], acc, 0, 0, 0);
+      return acc;
+    };
+    // Horizontal 3-max of a conv row, H[m] = max(local cols 2m, 2m+1, 2m+2):
+    // half 0 takes column 16 from half 1; quarter 0's column 0 is conv column
+    // -1 (pool padding).  Half 1's H[6], H[7] and half 0's beyond m=7 are unused.
+    auto hpool = [&](v16i c, int (&H)[8]) {
+      unsigned x0 = (unsigned)c[0], c16 = (unsigned)c[0];
+      swap32s(x0, c16);  // lanes 0-31: c16 = lanes 32-63's c[0]
+      const int c0v = (q == 0 && lh == 0) ? kIntMin : c[0];
+      H[0] = max3i(c0v, c[1], c[2]);
+#pragma unroll
+      for (int m = 1; m < 7; ++m) H[m] = max3i(c[2 * m], c[2 * m + 1], c[2 * m + 2]);
+      H[7] = max3i(c[14], c[15], (int)c16);
+    };
+
+    // ---- prologue: pairs 0 .. SLA in flight (the ring's SLA+1 slots);
+    // convert pairs 0..2 (super rows 2py0-3 .. 2py0+2) once landed, then
+    // issue pairs SLA+1, SLA+2 into the freed slots; H of conv row 2py0-1.
+    for (int k = 0; k <= SLA; ++k) issue_pair(k);
+    if (D == 2)
+      wait_vm_const<2 * (SLA - 2)>();
+    else
+      wait_vm_const<SLA - 2>();
+    __builtin_amdgcn_s_barrier();
+    convert_pair(0);
+    convert_pair(1);
+    convert_pair(2);
+    __syncthreads();
+    issue_pair(SLA + 1);
+    issue_pair(SLA + 2);
+    int Hp[8];
+    if (py0 == 0) {
+#pragma unroll
+      for (int m = 0; m < 8; ++m) Hp[m] = kIntMin;  // conv row -1: pool padding
+    } else {
+      hpool(conv_row(2 * py0 - 1), Hp);
     }
+
+    for (int p = py0; p < py1; ++p) {
+      const int t = p - py0;
+      // Pair t+3 (super rows 2p+3, 2p+4) has landed once only the younger VM
+      // ops remain: pairs t+4 .. t+2+SLA and the output stores of the last
+      // min(t, SLA) steps.
+      wait_vm((SLA - 1) * D + (t < SLA ? t : SLA));
+      __builtin_amdgcn_s_barrier();
+      convert_pair(t + 3);
+      issue_pair(t + 3 + SLA);
+
+      int He[8], Ho[8];
+      hpool(conv_row(2 * p), He);
+      hpool(conv_row(2 * p + 1), Ho);
+      // vertical max, epilogue on the pooled values, bytes -> staging [16 px][32 oc]
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int v = max3i(Hp[m], He[m], Ho[m]);
+        Hp[m] = Ho[m];
+        const float y = __builtin_fmaf((float)v, al, be);
+        const unsigned u = __float_as_uint(__builtin_amdgcn_fmed3f(y, 0.f, 127.f) + 12582912.0f);
+        stg[(m + 8 * lh) * 32 + lr] = (int8_t)u;
+      }
+      // 14 pooled columns x 32 channels = 28 x 16 B (written by this wave: LDS is in order)
+      const int pxl = lane >> 1, hf = lane & 1;
+      const v4i o = *(const v4i*)(stg + pxl * 32 + hf * 16);
+      if (lane < 28) *(v4i*)(a.y + (((size_t)n * 56 + p) * 56 + 14 * q + pxl) * 64 + ot * 32 + hf * 16) = o;
+    }
+    wait_vm0();
+    __syncthreads();  // ring reuse by the next item
   }
 }
 
@@ -218,26 +248,38 @@ int num_cus_stem() {
 
 size_t stem_packed_bytes() { return 64 * 256; }
 
-// OIHW int8 q[64][3][7][7] -> [64][ky 4][kx 4][dy 2][dx 2][c 4], kh = 2ky+dy-1.
-void pack_stem_weights(const int8_t* q, int8_t* out) {
+// OIHW int8 q[64][3][7][7] -> [64][ky 4][kx 4][dy 2][dx 2][c 4] with
+// kh = 2ky+dy-1, kw = 2kx+dx-1; rows of channels with alpha < 0 are negated
+// and |alpha| returned, which keeps the fused stem's pool-before-epilogue exact.
+void pack_stem_weights(const int8_t* q, const float* alpha, int8_t* out, float* alpha_abs) {
   for (int i = 0; i < 64 * 256; ++i) out[i] = 0;
-  for (int o = 0; o < 64; ++o)
+  for (int o = 0; o < 64; ++o) {
+    const bool neg = alpha[o] < 0.f;
+    alpha_abs[o] = neg ? -alpha[o] : alpha[o];
     for (int ky = 0; ky < 4; ++ky)
       for (int kx = 0; kx < 4; ++kx)
         for (int dy = 0; dy < 2; ++dy)
           for (int dx = 0; dx < 2; ++dx) {
             const int kh = 2 * ky + dy - 1, kw = 2 * kx + dx - 1;
             if (kh < 0 || kw < 0) continue;
-            for (int c = 0; c < 3; ++c)
-              out[o * 256 + (((ky * 4 + kx) * 2 + dy) * 2 + dx) * 4 + c] = q[((o * 3 + c) * 7 + kh) * 7 + kw];
+            for (int c = 0; c < 3; ++c) {
+              const int v = q[((o * 3 + c) * 7 + kh) * 7 + kw];
+              out[o * 256 + (((ky * 4 + kx) * 2 + dy) * 2 + dx) * 4 + c] = (int8_t)(neg ? -v : v);
+            }
           }
+  }
 }
 
 hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float* alpha, const float* beta,
                              float inv_s, int8_t* y, hipStream_t s) {
-  StemArgs a{x, w, alpha, beta, y, inv_s, N, debug_bits()};
-  const int nb = N * (56 / PR), ncu = num_cus_stem();
-  hipLaunchKernelGGL(stem_fused_kernel, dim3(nb < ncu ? nb : ncu), dim3(NTH), 0, s, a);
+  const int ncu = num_cus_stem();
+  int nb = (ncu + N - 1) / N;  // bands per image so that every CU gets an item
+  nb = nb < 1 ? 1 : (nb > 14 ? 14 : nb);
+  const int R = (56 + nb - 1) / nb;
+  nb = (56 + R - 1) / R;
+  StemArgs a{x, w, alpha, beta, y, inv_s, N, nb, R};
+  const int items = N * nb;
+  hipLaunchKernelGGL(stem_fused_kernel, dim3(items < ncu ? items : ncu), dim3(SNW * 64), 0, s, a);
   return hipGetLastError();
 }
 

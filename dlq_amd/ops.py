@@ -74,14 +74,17 @@ def pack_linear_weights(q: np.ndarray, K: int | None = None) -> np.ndarray:
     return pack_conv_weights(np.ascontiguousarray(q, np.int8).reshape(OC, IC, 1, 1), K or IC, 1, 1, 0)
 
 
-def pack_stem_weights(q_oihw: np.ndarray) -> np.ndarray:
-    """conv1 weights [64][3][7][7] int8 -> the fused stem's space-to-depth image."""
+def pack_stem_weights(q_oihw: np.ndarray, alpha: np.ndarray):
+    """conv1 weights [64][3][7][7] int8 + conv1 alpha[64] -> (the fused stem's
+    space-to-depth image, |alpha|) for stem_fused_s8 (see include/dlq.h)."""
     q = np.ascontiguousarray(q_oihw, np.int8)
-    if q.shape != (64, 3, 7, 7):
-        raise ValueError(f"stem weights must be [64,3,7,7], got {q.shape}")
+    al = np.ascontiguousarray(alpha, np.float32)
+    if q.shape != (64, 3, 7, 7) or al.shape != (64,):
+        raise ValueError(f"stem weights must be [64,3,7,7] with alpha[64], got {q.shape}, {al.shape}")
     out = np.empty(lib.dlq_stem_packed_bytes(), np.int8)
-    check(lib.dlq_pack_stem_weights_s8(ptr(q), ptr(out)), "pack_stem_weights")
-    return out
+    al_out = np.empty(64, np.float32)
+    check(lib.dlq_pack_stem_weights_s8(ptr(q), ptr(al), ptr(out), ptr(al_out)), "pack_stem_weights")
+    return out, al_out
 
 
 def pad_vec(v, n):
@@ -137,7 +140,8 @@ def conv2d_nhwc_s8(x: torch.Tensor, w_packed: torch.Tensor, OC: int, k: int, str
 def stem_fused_s8(x: torch.Tensor, w_stem: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor,
                   in_scale: float) -> torch.Tensor:
     """quantise + conv1 7x7/s2 + BN/ReLU/requant + maxpool 3x3/s2 in one launch:
-    fp32 NCHW [N,3,224,224] -> int8 NHWC [N,56,56,64] (alpha/beta in conv1's grid)."""
+    fp32 NCHW [N,3,224,224] -> int8 NHWC [N,56,56,64]; w_stem, alpha from
+    pack_stem_weights, beta = conv1's beta (output-grid units)."""
     _dev(x, torch.float32)
     N = x.shape[0]
     if tuple(x.shape[1:]) != (3, 224, 224):

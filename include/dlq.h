@@ -131,12 +131,15 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
  * maxpool3x3s2p1(requant(ReLU(BN(conv7x7s2p3(quant(x)))))).  One launch
  * replaces the input upload + conv1 + bn1 + relu + maxpool sequence of
  * RK/runtime/infer_e2e.cu:255-293; the 112x112 conv1 output never reaches
- * HBM.  w_stem = dlq_pack_stem_weights_s8 image (64 x 256 B: 7x7x3 taps
- * re-indexed for a 2x2 space-to-depth input), alpha/beta[64] in conv1's
- * output-grid units, inv_s = 1/input scale.  Bit-identical to
- * dlq_quantize_nchw_to_nhwc_s8 + dlq_conv2d_nhwc_s8 (stem) + maxpool. */
+ * HBM.  dlq_pack_stem_weights_s8 turns the int8 OIHW conv1 weights and conv1's
+ * alpha[64] (output-grid units, dlq_fold_bn) into the kernel's image (64 x
+ * 256 B: 7x7x3 taps re-indexed for a 2x2 space-to-depth input; rows of
+ * channels with alpha < 0 negated) and alpha_packed = |alpha|; pass
+ * alpha_packed and the unchanged beta[64] to dlq_stem_fused_s8 (inv_s =
+ * 1/input scale).  Bit-identical to dlq_quantize_nchw_to_nhwc_s8 +
+ * dlq_conv2d_nhwc_s8 (stem, alpha/beta) + dlq_maxpool2d_3x3_s2p1_nhwc_s8. */
 size_t dlq_stem_packed_bytes(void);
-int dlq_pack_stem_weights_s8(const int8_t* q_oihw, int8_t* packed);
+int dlq_pack_stem_weights_s8(const int8_t* q_oihw, const float* alpha, int8_t* packed, float* alpha_packed);
 int dlq_stem_fused_s8(const float* x, int N, const int8_t* w_stem, const float* alpha, const float* beta,
                       float inv_s, int8_t* y, void* stream);
 

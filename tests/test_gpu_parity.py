@@ -95,7 +95,7 @@ def test_conv_fused_epilogue_bitexact(gpu, shape, residual):
     assert np.array_equal(got, ref), f"{name}: {np.count_nonzero(got != ref)} int8 mismatches"
 
 
-@pytest.mark.parametrize("N", [1, 3])
+@pytest.mark.parametrize("N", [1, 3, 37])
 def test_stem_fused_bitexact(gpu, N):
     """quantise + conv1 7x7/s2 + BN/ReLU/requant + maxpool as ONE launch
     (infer_e2e.cu:259-301) == the oracle's four separate steps."""
@@ -105,13 +105,15 @@ def test_stem_fused_bitexact(gpu, N):
     x[0, :, 0, :6] = [[0.5, 1.5, -2.5, 1e9, -1e9, 0.0]] * 3  # ties, saturation, the padded border
     x[N - 1, 2, 223, 218:] = [-0.5, 2.5, 1e9, -1e9, 3.5, 0.0]
     w, bn = rand_conv(rng, 64, 3, 7)
+    bn[0][::3] *= -1  # some negative BN gammas -> negative alpha (the packer's sign fold)
     wq, sw = O.quantize_weights_s8(w)
     s_in, s_y = 2.64 / 127, 0.043
     alpha, beta = O.fold_bn(s_in, sw, bn, s_y)
+    assert (alpha < 0).any() and (alpha > 0).any()
     xq = O.quantize_f32_s8(x, s_in)
     ref = O.maxpool_s8(O.epilogue_s8(O.conv_s8_acc(xq, wq, 2, 3), alpha, beta, None, 0.0, True))
-    wst = _cuda(ops.pack_stem_weights(wq))
-    y = ops.stem_fused_s8(_cuda(x), wst, _cuda(alpha), _cuda(beta), s_in)
+    wst, al_p = ops.pack_stem_weights(wq, alpha)
+    y = ops.stem_fused_s8(_cuda(x), _cuda(wst), _cuda(al_p), _cuda(beta), s_in)
     got = nhwc_to_nchw(y.cpu().numpy())
     assert np.array_equal(got, ref), f"{np.count_nonzero(got != ref)} int8 mismatches"
 

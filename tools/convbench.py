@@ -60,8 +60,9 @@ def main():
     if "stemf" in args.only.split(","):
         x = torch.randn(args.batch, 3, 224, 224, device="cuda")
         q = rng.integers(-127, 128, size=(64, 3, 7, 7), dtype=np.int8)
-        w = torch.from_numpy(ops.pack_stem_weights(q)).cuda()
-        alpha = torch.full((64,), 1e-3, device="cuda")
+        wp, alp = ops.pack_stem_weights(q, np.full(64, 1e-3, np.float32))
+        w = torch.from_numpy(wp).cuda()
+        alpha = torch.from_numpy(alp).cuda()
         beta = torch.zeros(64, device="cuda")
         bench("stemf", lambda: ops.stem_fused_s8(x, w, alpha, beta, 0.02), args.iters, tag,
               args.batch * 112 * 112 * 64 * 3 * 49)
