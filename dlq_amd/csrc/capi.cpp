@@ -109,7 +109,8 @@ bool wide_layout(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, in
     const char* e = std::getenv("DLQ_CONV_V1");
     return e && e[0] == '1';
   }();
-  return !force_v1 && conv3x3w_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW);
+  return !force_v1 && (conv3x3w_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW) ||
+                       conv3x3s2_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW));
 }
 
 size_t packed_bytes_for(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW) {
@@ -189,9 +190,11 @@ int dlq_quantize_rows_s8(const float* x, int rows, int cols, int ldy, float inv_
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, hipGetErrorString(e));
 }
 
-int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
-                       const float* alpha, const float* beta, const int8_t* residual,
-                       float res_scale, int relu, int out_kind, void* y, void* stream) {
+namespace {
+// Validation + ConvArgs of one conv launch (shared by the conv entry points).
+int conv_args(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
+              const float* beta, const int8_t* residual, float res_scale, int relu, int out_kind, void* y,
+              ConvArgs& a, bool& wide) {
   if (!d || !x || !w_packed || !y) return fail(DLQ_ERR_ARG, "conv2d: null pointer");
   if (out_kind < 0 || out_kind > 2) return fail(DLQ_ERR_ARG, "conv2d: bad out_kind");
   if (out_kind != DLQ_OUT_S32 && (!alpha || !beta)) return fail(DLQ_ERR_ARG, "conv2d: alpha/beta required");
@@ -200,9 +203,10 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
     return fail(DLQ_ERR_ARG, "conv2d: bad shape");
   if (packed_bytes_for(DLQ_DESC_GEOM(d)) == 0)
     return fail(DLQ_ERR_ARG, "conv2d: unsupported C (need C%64==0, or C==4 with a 7x7 kernel)");
-  const bool wide = wide_layout(DLQ_DESC_GEOM(d));
+  wide = wide_layout(DLQ_DESC_GEOM(d));
   if (wide && out_kind == DLQ_OUT_F32) return fail(DLQ_ERR_ARG, "conv2d: this shape supports int8 / int32 output");
-  ConvArgs a{};
+  if (wide && d->sH == 2 && residual) return fail(DLQ_ERR_ARG, "conv2d: stride-2 3x3 takes no residual");
+  a = ConvArgs{};
   a.x = x; a.w = w_packed; a.alpha = alpha; a.beta = beta; a.res = residual; a.y = y;
   a.s_res = res_scale;
   a.N = d->N; a.H = d->H; a.W = d->W; a.C = d->C;
@@ -224,9 +228,49 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
   if (is_stem(a.C, a.kH, a.kW) && (residual || out_kind == DLQ_OUT_F32))
     return fail(DLQ_ERR_ARG, "conv2d: stem supports int8 (no residual) or int32 output");
   a.P = (int)P;
+  return DLQ_OK;
+}
+}  // namespace
+
+int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
+                       const float* alpha, const float* beta, const int8_t* residual,
+                       float res_scale, int relu, int out_kind, void* y, void* stream) {
+  ConvArgs a;
+  bool wide = false;
+  int rc = conv_args(d, x, w_packed, alpha, beta, residual, res_scale, relu, out_kind, y, a, wide);
+  if (rc) return rc;
   if (a.P == 0) return DLQ_OK;
-  hipError_t e = wide ? launch_conv3x3w(a, (hipStream_t)stream) : launch_conv(a, (hipStream_t)stream);
+  hipError_t e = !wide ? launch_conv(a, (hipStream_t)stream)
+                 : a.sH == 2 ? launch_conv3x3s2(a, nullptr, nullptr, nullptr, nullptr, (hipStream_t)stream)
+                             : launch_conv3x3w(a, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d launch: ") + hipGetErrorString(e));
+}
+
+size_t dlq_downsample_packed_bytes(int OC, int C) {
+  return (OC > 0 && C > 0 && C % 32 == 0) ? downsample_packed_bytes(OC, C) : 0;
+}
+
+int dlq_pack_downsample_weights_s8(const int8_t* q, int OC, int IC, int C, int8_t* packed) {
+  if (!q || !packed || OC <= 0 || IC <= 0 || IC > C || C % 32)
+    return fail(DLQ_ERR_ARG, "pack_downsample_weights: bad args (IC <= C, C % 32 == 0)");
+  downsample_pack(q, OC, IC, C, packed);
+  return DLQ_OK;
+}
+
+int dlq_conv2d_s2_ds_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
+                             const float* alpha, const float* beta, const int8_t* w_ds, const float* alpha_ds,
+                             const float* beta_ds, int8_t* y, int8_t* y_ds, void* stream) {
+  if (!d || !conv3x3s2_shape(DLQ_DESC_GEOM(d)))
+    return fail(DLQ_ERR_ARG, "conv2d_s2_ds: needs a 3x3/s2/p1 C->2C conv at 56x56x64, 28x28x128 or 14x14x256");
+  if (!w_ds || !alpha_ds || !beta_ds || !y_ds) return fail(DLQ_ERR_ARG, "conv2d_s2_ds: null pointer");
+  ConvArgs a;
+  bool wide = false;
+  int rc = conv_args(d, x, w_packed, alpha, beta, nullptr, 0.f, 1, DLQ_OUT_S8, y, a, wide);
+  if (rc) return rc;
+  if (!wide) return fail(DLQ_ERR_STATE, "conv2d_s2_ds: disabled by DLQ_CONV_V1");
+  if (a.P == 0) return DLQ_OK;
+  hipError_t e = launch_conv3x3s2(a, w_ds, alpha_ds, beta_ds, y_ds, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d_s2_ds launch: ") + hipGetErrorString(e));
 }
 
 size_t dlq_stem_packed_bytes(void) { return stem_packed_bytes(); }

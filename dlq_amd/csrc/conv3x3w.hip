@@ -48,8 +48,13 @@ __device__ unsigned long long g_stamps[256 * 8 * 64];
 
 constexpr int WTM = 128;                  // oc per item
 constexpr int WTN = 256;                  // px per item
-constexpr int WNW = 8;                    // waves
-constexpr int WLW = 8;                    // of which issue the LDS-DMA (waves 0..WLW-1)
+constexpr int WFM = 2;                    // 32-oc MFMA tiles per wave
+constexpr int WFN = 2;                    // 32-px MFMA tiles per wave
+constexpr int WMW = WTM / (32 * WFM);     // waves along oc
+constexpr int WNW = WMW * (WTN / (32 * WFN));  // waves: 2 per SIMD, wave tile 64 oc x 64 px
+// (a 4-wave 128 oc x 64 px tiling halves nothing that matters: one wave per
+//  SIMD cannot overlap LDS latency with MFMAs; measured 1.4x slower)
+constexpr int WLW = WNW;                  // of which issue the LDS-DMA (waves 0..WLW-1)
 constexpr int WSC = 32;                   // input channels per stage
 constexpr int WPITCH = 9 * WSC + 16;      // weight row pitch (304 = 19 x 16 B: odd -> conflict-free)
 constexpr int WSTAGE_W = WTM * WPITCH;    // 38,912 B = 38 LDS-DMA pieces
@@ -66,32 +71,6 @@ struct WPatch {
   static constexpr int PBYTES = PIECES * 1024;
 };
 
-// v_permlane32_swap_b32: lanes 32-63 of x <-> lanes 0-31 of y.
-__device__ __forceinline__ void swap32(unsigned& x, unsigned& y) {
-  const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
-  x = r[0];
-  y = r[1];
-}
-
-// 16-byte global load the compiler does not track: its completion is awaited
-// only by an explicit counted wait (see the epilogue), so hipcc's waitcnt pass
-// cannot turn the loop-carried load into a vmcnt(0) drain of the DMA ring.
-__device__ __forceinline__ v4i gload16_untracked(const void* p) {
-  v4i r;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
-  return r;
-}
-
-// One LDS-DMA piece (1 KiB: 16 B per lane to lds_base + 16*lane) issued from
-// asm.  The builtin carries an LDS memory operand, which hipcc's waitcnt pass
-// treats as a possible FLAT-LDS access: every later ds_read wait then becomes
-// lgkmcnt(0), draining the fragment prefetch.  Completion is covered by the
-// kernel's explicit vmcnt counts + barrier; the "memory" clobbers keep the
-// compiler from moving LDS accesses across it.
-__device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_addr) {
-  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
-  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "{m0}"(m0) : "memory");
-}
 
 // OUT: 0 = int8 (fused epilogue), 2 = int32 accumulators.  XB: timing
 // experiments for tools/probe (0 in the library): 1 no MFMA, 2 patch pieces
@@ -109,8 +88,8 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
   constexpr int WP = WSTAGE_W / 1024, NPIECE = WP + G::PIECES;
   constexpr int DPW = (NPIECE + WLW - 1) / WLW;  // LDS-DMA instructions per loader wave per stage
   static_assert(DPW <= 18, "at most two DMA pieces per tap");
-  constexpr int LOADS = (OUT == 0 && RES) ? 4 : 0;  // epilogue residual loads per wave
-  constexpr int STORES = OUT == 0 ? 4 : 16;         // epilogue stores per wave
+  constexpr int LOADS = (OUT == 0 && RES) ? WFM * WFN : 0;  // epilogue residual loads per wave
+  constexpr int STORES = OUT == 0 ? WFM * WFN : 4 * WFM * WFN;  // epilogue stores per wave
   constexpr int OFF_AB = WRING * STAGE;
   constexpr int LDS_TOTAL = OFF_AB + 2 * C * 4;
   static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
@@ -119,7 +98,7 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 31, lh = lane >> 5;
-  const int wm = wave & 1, wn = wave >> 1;  // 64-oc half, 64-px quarter of the item
+  const int wm = wave % WMW, wn = wave / WMW;  // wave's oc group and px group in the item
   const bool loader = wave < WLW;
   const int n_ot = a.OCp / WTM;
   const int NI = n_ot * ((a.P + WTN - 1) / WTN);
@@ -202,12 +181,12 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
   };
 
   // ---- compute side
-  int a_off[2];  // weight fragment: row wm*64 + fm*32 + lr, half lh (+ tap*32)
+  int a_off[WFM];  // weight fragment: row wm*32*WFM + fm*32 + lr, half lh (+ tap*32)
 #pragma unroll
-  for (int fm = 0; fm < 2; ++fm) a_off[fm] = (wm * 64 + fm * 32 + lr) * WPITCH + lh * 16;
-  int rel_b[2][9];  // patch fragment offset within a slot per (pixel tile, tap); ZREL if outside
-  v16i acc[2][2];
-  v4i rq[2][2] = {};  // residual in the store layout, loaded one stage early
+  for (int fm = 0; fm < WFM; ++fm) a_off[fm] = (wm * 32 * WFM + fm * 32 + lr) * WPITCH + lh * 16;
+  int rel_b[WFN][9];  // patch fragment offset within a slot per (pixel tile, tap); ZREL if outside
+  v16i acc[WFM][WFN];
+  v4i rq[WFM][WFN] = {};  // residual in the store layout, loaded one stage early
   int cur_ot = 0, cur_p0 = 0;
 
   if (loader) {
@@ -248,10 +227,10 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
       item_of(li, cur_ot, cur_p0);
       const PatchTile cur = patch_tile(cur_p0, min(cur_p0 + WTN, a.P), W, H);
 #pragma unroll
-      for (int fn = 0; fn < 2; ++fn) {
+      for (int fn = 0; fn < WFN; ++fn) {
         int base;
         unsigned m;
-        patch_pixel(cur, cur_p0 + wn * 64 + fn * 32 + lr, W, H, base, m);
+        patch_pixel(cur, cur_p0 + wn * 32 * WFN + fn * 32 + lr, W, H, base, m);
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
           const int q = base + (tap / 3) * W + (tap % 3) - 1;
@@ -260,9 +239,9 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
         }
       }
 #pragma unroll
-      for (int fm = 0; fm < 2; ++fm)
+      for (int fm = 0; fm < WFM; ++fm)
 #pragma unroll
-        for (int fn = 0; fn < 2; ++fn) acc[fm][fn] = v16i{0};
+        for (int fn = 0; fn < WFN; ++fn) acc[fm][fn] = v16i{0};
     }
     // Residual of the item that ends at stage s+1, before stage s+2's DMA.
     if constexpr (LOADS > 0) {
@@ -270,11 +249,11 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
         int ot, p0;
         item_of(li, ot, p0);
 #pragma unroll
-        for (int fm = 0; fm < 2; ++fm)
+        for (int fm = 0; fm < WFM; ++fm)
 #pragma unroll
-          for (int fn = 0; fn < 2; ++fn) {
-            const int p = p0 + wn * 64 + fn * 32 + lr;
-            const size_t off = p < a.P ? (size_t)p * a.OC + ot * WTM + wm * 64 + fm * 32 + lh * 16 : 0;
+          for (int fn = 0; fn < WFN; ++fn) {
+            const int p = p0 + wn * 32 * WFN + fn * 32 + lr;
+            const size_t off = p < a.P ? (size_t)p * a.OC + ot * WTM + wm * 32 * WFM + fm * 32 + lh * 16 : 0;
             rq[fm][fn] = gload16_untracked(a.res + off);
           }
       }
@@ -284,12 +263,12 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
     // 9 taps x one 32-deep k-step.  Fragments are read two taps ahead; stage
     // s+2's DMA pieces go out one per tap between the MFMAs.
     const int sbase = (s % WRING) * STAGE;
-    v4i fa[3][2], fb[3][2];
+    v4i fa[3][WFM], fb[3][WFN];
     auto load_tap = [&](int tap, int buf) {
 #pragma unroll
-      for (int fm = 0; fm < 2; ++fm) fa[buf][fm] = *(const v4i*)(lds + sbase + a_off[fm] + tap * 32);
+      for (int fm = 0; fm < WFM; ++fm) fa[buf][fm] = *(const v4i*)(lds + sbase + a_off[fm] + tap * 32);
 #pragma unroll
-      for (int fn = 0; fn < 2; ++fn) fb[buf][fn] = *(const v4i*)(lds + sbase + rel_b[fn][tap]);
+      for (int fn = 0; fn < WFN; ++fn) fb[buf][fn] = *(const v4i*)(lds + sbase + rel_b[fn][tap]);
     };
     // DMA pieces of stage s+2 per tap (loader waves): pieces [t*DPW/9, (t+1)*DPW/9)
     auto run_taps = [&](auto mfma_on, auto ld) {
@@ -307,29 +286,33 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
         const int bu = tap % 3;
         if constexpr (decltype(mfma_on)::value) {
 #pragma unroll
-          for (int fm = 0; fm < 2; ++fm)
+          for (int fm = 0; fm < WFM; ++fm)
 #pragma unroll
-            for (int fn = 0; fn < 2; ++fn)
+            for (int fn = 0; fn < WFN; ++fn)
               acc[fm][fn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu][fm], fb[bu][fn], acc[fm][fn], 0, 0, 0);
         } else {
-          asm volatile("" ::"v"(fa[bu][0]), "v"(fa[bu][1]), "v"(fb[bu][0]), "v"(fb[bu][1]));
+#pragma unroll
+          for (int fm = 0; fm < WFM; ++fm) asm volatile("" ::"v"(fa[bu][fm]));
+#pragma unroll
+          for (int fn = 0; fn < WFN; ++fn) asm volatile("" ::"v"(fb[bu][fn]));
         }
+        // interleave: the next fragments' ds_reads and this tap's DMA pieces between the MFMAs
         const int nv = LD ? k1 - k0 : 0;
+        constexpr int NR = WFM + WFN, NM = WFM * WFN;
         if (tap + 2 < 9) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          if (nv > 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (LDS-DMA piece)
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          if (nv > 1) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+          for (int i = 0; i < NM; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            if (i < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            if (i == 2 && nv > 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (LDS-DMA)
+            if (i == 5 && nv > 1) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            if (i == 7 && nv > 2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          }
         } else {
           if (nv > 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
           if (nv > 1) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+          if (nv > 2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
         }
       }
     };
@@ -344,14 +327,14 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
     // ---- fused epilogue of the item ----
     if constexpr (OUT == 2) {
 #pragma unroll
-      for (int fn = 0; fn < 2; ++fn) {
-        const int p = cur_p0 + wn * 64 + fn * 32 + lr;
+      for (int fn = 0; fn < WFN; ++fn) {
+        const int p = cur_p0 + wn * 32 * WFN + fn * 32 + lr;
         const bool keep = p < a.P;
 #pragma unroll
-        for (int fm = 0; fm < 2; ++fm)
+        for (int fm = 0; fm < WFM; ++fm)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const int oc = cur_ot * WTM + wm * 64 + fm * 32 + 8 * g + 4 * lh;
+            const int oc = cur_ot * WTM + wm * 32 * WFM + fm * 32 + 8 * g + 4 * lh;
             v4i* dst = keep ? (v4i*)((int*)a.y + (size_t)p * a.OC + oc) : (v4i*)(g_trash_w + lane * 16);
             *dst = v4i{acc[fm][fn][4 * g], acc[fm][fn][4 * g + 1], acc[fm][fn][4 * g + 2], acc[fm][fn][4 * g + 3]};
           }
@@ -359,6 +342,7 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
     } else {
       if constexpr (RES) {
         // issued at stage s-1 before the pieces of stages s+1 and s+2
+        static_assert(WFM == 2 && WFN == 2, "the residual wait below names 4 registers");
         if (loader)
           asm volatile("s_waitcnt vmcnt(%4)"
                        : "+v"(rq[0][0]), "+v"(rq[0][1]), "+v"(rq[1][0]), "+v"(rq[1][1])
@@ -372,12 +356,12 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
       }
       const float lo = a.relu ? 0.f : -127.f;
 #pragma unroll
-      for (int fm = 0; fm < 2; ++fm) {
+      for (int fm = 0; fm < WFM; ++fm) {
         // alpha/beta of this lane's 16 channels (MFMA layout), read as ints
         float al[4][4], be[4][4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int oc = cur_ot * WTM + wm * 64 + fm * 32 + 8 * g + 4 * lh;
+          const int oc = cur_ot * WTM + wm * 32 * WFM + fm * 32 + 8 * g + 4 * lh;
           const v4i a4 = *(const v4i*)(lds + OFF_AB + oc * 4);
           const v4i b4 = *(const v4i*)(lds + OFF_AB + (C + oc) * 4);
 #pragma unroll
@@ -387,7 +371,7 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
           }
         }
 #pragma unroll
-        for (int fn = 0; fn < 2; ++fn) {
+        for (int fn = 0; fn < WFN; ++fn) {
           unsigned r[4] = {0, 0, 0, 0};
           if constexpr (RES) {
             // store layout -> MFMA layout: (r0,r1) and (r2,r3) swaps give g = 0,2 and 1,3
@@ -413,9 +397,9 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
           // MFMA layout -> 16 contiguous channels per lane
           swap32(q[0], q[2]);
           swap32(q[1], q[3]);
-          const int p = cur_p0 + wn * 64 + fn * 32 + lr;
+          const int p = cur_p0 + wn * 32 * WFN + fn * 32 + lr;
           const bool keep = p < a.P;
-          v4i* dst = keep ? (v4i*)((int8_t*)a.y + (size_t)p * a.OC + cur_ot * WTM + wm * 64 + fm * 32 + lh * 16)
+          v4i* dst = keep ? (v4i*)((int8_t*)a.y + (size_t)p * a.OC + cur_ot * WTM + wm * 32 * WFM + fm * 32 + lh * 16)
                           : (v4i*)(g_trash_w + lane * 16);
           *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
         }

@@ -56,6 +56,46 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
 
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// One LDS-DMA piece (1 KiB: 16 B per lane to lds_addr + 16*lane) issued from
+// asm.  The builtin carries an LDS memory operand, which hipcc's waitcnt pass
+// treats as a possible FLAT-LDS access: every later ds_read wait then becomes
+// lgkmcnt(0), draining the fragment prefetch.  Completion must be covered by
+// the caller's explicit vmcnt counts + barrier.
+__device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_addr) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "{m0}"(m0) : "memory");
+}
+
+// LDS byte address of a __shared__ pointer (for M0).
+__device__ __forceinline__ unsigned lds_addr32(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// v_permlane32_swap_b32: lanes 32-63 of x <-> lanes 0-31 of y.
+__device__ __forceinline__ void swap32(unsigned& x, unsigned& y) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+  x = r[0];
+  y = r[1];
+}
+
+// 16-byte global load the compiler does not track: its completion is awaited
+// only by an explicit counted wait, so hipcc's waitcnt pass cannot turn a
+// loop-carried load into a vmcnt(0) drain of an LDS-DMA ring.
+__device__ __forceinline__ v4i gload16_untracked(const void* p) {
+  v4i r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+
+// MFMA-layout <-> store-layout exchange for a 32x32 int8 output tile (see
+// conv3x3w.hip): q[g] holds channels 8g + 4h .. +3 of this lane's pixel (h =
+// lane half); afterwards {q0, q2, q1, q3} are channels 16h .. 16h+15.
+__device__ __forceinline__ v4i mfma_to_store16(unsigned q0, unsigned q1, unsigned q2, unsigned q3) {
+  swap32(q0, q2);
+  swap32(q1, q3);
+  return v4i{(int)q0, (int)q2, (int)q1, (int)q3};
+}
+
 // s_waitcnt vmcnt(N) expcnt(7) lgkmcnt(0) for a wave-uniform runtime N <= 63
 // (gfx9 encoding: vmcnt[3:0] in bits 3:0, vmcnt[5:4] in bits 15:14).  A
 // builtin per case so hipcc's waitcnt pass sees every wait.

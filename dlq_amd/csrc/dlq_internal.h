@@ -45,6 +45,13 @@ bool conv3x3w_shape(int C, int OC, int H, int W, int kH, int kW, int sH, int sW,
 size_t conv3x3w_packed_bytes(int OC, int C);
 void conv3x3w_pack(const int8_t* q_oihw, int OC, int IC, int C, int8_t* out);
 hipError_t launch_conv3x3w(const ConvArgs& a, hipStream_t s);
+// Stride-2 3x3 convs (conv3x3s2.hip), wide weight layout, optional fused 1x1/s2
+// downsample (w_ds == nullptr: conv only).
+bool conv3x3s2_shape(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW);
+size_t downsample_packed_bytes(int OC, int C);
+void downsample_pack(const int8_t* q_oc_ic, int OC, int IC, int C, int8_t* out);
+hipError_t launch_conv3x3s2(const ConvArgs& a, const int8_t* w_ds, const float* alpha_ds, const float* beta_ds,
+                            int8_t* y_ds, hipStream_t s);
 // Fused stem (stem.hip): quantise + conv1 7x7/s2 + BN/ReLU/requant + maxpool.
 size_t stem_packed_bytes();
 void pack_stem_weights(const int8_t* q_oihw, const float* alpha, int8_t* out, float* alpha_abs);

@@ -38,6 +38,7 @@ struct ConvLayer {
   int IC = 0, OC = 0, k = 0, s = 1, p = 0, Cstore = 0;
   int H = 0;            // input height = width
   int8_t* w = nullptr;  // packed weights (device)
+  int8_t* wf = nullptr; // downsample convs: the fused stride-2 kernel's layout (dlq_pack_downsample_weights_s8)
   float* alpha = nullptr;
   float* beta = nullptr;
 };
@@ -167,7 +168,7 @@ int dev_alloc(dlq_resnet18* m, T** p, size_t bytes) {
 void free_all(dlq_resnet18* m) {
   for (void* p : m->allocs) (void)hipFree(p);
   m->allocs.clear();
-  for (auto& c : m->convs) { c.w = nullptr; c.alpha = nullptr; c.beta = nullptr; }
+  for (auto& c : m->convs) { c.w = nullptr; c.wf = nullptr; c.alpha = nullptr; c.beta = nullptr; }
   m->fc_w = nullptr; m->fc_alpha = m->fc_beta = nullptr;
   m->xq = m->c1 = m->gq = m->stem_w = nullptr;
   m->stem_alpha = nullptr;
@@ -208,17 +209,32 @@ int basic_block_forward(const dlq_resnet18* m, const Block& b, const int8_t* in,
                         int W, int8_t* h, int8_t* dsb, int8_t* out, hipStream_t s, int* OH,
                         int* OW) {
   int h1, w1, h2, w2;
-  int rc = conv2d_nhwc_s8(m, m->convs[b.c1], in, N, H, W, nullptr, 0.f, true, h, s, &h1, &w1);
-  if (rc) return rc;
+  const ConvLayer& c1 = m->convs[b.c1];
   const int8_t* skip = in;
-  float s_skip = m->scales.at(m->convs[b.c1].in_site);
-  if (b.down) {
-    int hd, wd;
-    rc = conv2d_nhwc_s8(m, m->convs[b.ds], in, N, H, W, nullptr, 0.f, false, dsb, s, &hd, &wd);
+  float s_skip = m->scales.at(c1.in_site);
+  int rc;
+  if (b.down && m->convs[b.ds].wf && conv3x3s2_shape(c1.Cstore, c1.OC, H, W, 3, 3, 2, 2, 1, 1) &&
+      wide_layout(c1.Cstore, c1.OC, H, W, 3, 3, 2, 2, 1, 1)) {
+    // conv1 (3x3/s2) and the 1x1/s2 downsample in one launch
+    const ConvLayer& ds = m->convs[b.ds];
+    dlq_conv_desc d{N, H, W, c1.Cstore, c1.OC, 3, 3, 2, 2, 1, 1};
+    rc = dlq_conv2d_s2_ds_nhwc_s8(&d, in, c1.w, c1.alpha, c1.beta, ds.wf, ds.alpha, ds.beta, h, dsb, s);
     if (rc) return rc;
-    if (hd != h1 || wd != w1) return fail(DLQ_ERR_STATE, "downsample shape mismatch");
+    h1 = out_dim(H, 3, 2, 1);
+    w1 = out_dim(W, 3, 2, 1);
     skip = dsb;
-    s_skip = m->scales.at(m->convs[b.ds].site);
+    s_skip = m->scales.at(ds.site);
+  } else {
+    rc = conv2d_nhwc_s8(m, c1, in, N, H, W, nullptr, 0.f, true, h, s, &h1, &w1);
+    if (rc) return rc;
+    if (b.down) {
+      int hd, wd;
+      rc = conv2d_nhwc_s8(m, m->convs[b.ds], in, N, H, W, nullptr, 0.f, false, dsb, s, &hd, &wd);
+      if (rc) return rc;
+      if (hd != h1 || wd != w1) return fail(DLQ_ERR_STATE, "downsample shape mismatch");
+      skip = dsb;
+      s_skip = m->scales.at(m->convs[b.ds].site);
+    }
   }
   rc = conv2d_nhwc_s8(m, m->convs[b.c2], h, N, h1, w1, skip, s_skip, true, out, s, &h2, &w2);
   *OH = h2;
@@ -368,6 +384,13 @@ int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
         (e = hipMemcpy(c.alpha, alpha.data(), ocp * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c.beta, beta.data(), ocp * 4, hipMemcpyHostToDevice)) != hipSuccess)
       return hip_fail(e, "weight upload");
+    if (c.k == 1 && c.s == 2 && c.Cstore % 32 == 0) {  // downsample: fused into the stride-2 conv1
+      std::vector<int8_t> fp(downsample_packed_bytes(c.OC, c.Cstore));
+      downsample_pack(q.data(), c.OC, c.IC, c.Cstore, fp.data());
+      if ((rc = dev_alloc(m, &c.wf, fp.size()))) return rc;
+      if ((e = hipMemcpy(c.wf, fp.data(), fp.size(), hipMemcpyHostToDevice)) != hipSuccess)
+        return hip_fail(e, "downsample weight upload");
+    }
     if (&c == &m->convs[m->stem]) {  // the fused stem's space-to-depth weight image
       std::vector<int8_t> sp(stem_packed_bytes());
       std::vector<float> sa(64);

@@ -56,22 +56,9 @@ struct StemArgs {
   int N, nb, R;        // batch, bands per image, pooled rows per band
 };
 
-__device__ __forceinline__ void swap32s(unsigned& x, unsigned& y) {
-  const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
-  x = r[0];
-  y = r[1];
-}
 
 __device__ __forceinline__ int max3i(int a, int b, int c) {
   return __builtin_elementwise_max(__builtin_elementwise_max(a, b), c);
-}
-
-// One LDS-DMA piece from asm: the builtin's LDS memory operand makes hipcc's
-// waitcnt pass drain every later ds_read with lgkmcnt(0) (see conv3x3w.hip).
-// Completion is covered by the explicit vmcnt counts + barrier below.
-__device__ __forceinline__ void glds16_stem(const void* gsrc, unsigned lds_addr) {
-  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
-  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "{m0}"(m0) : "memory");
 }
 
 __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
@@ -117,7 +104,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
           const bool ok = (unsigned)sr < 112u;
           const int l = lane < 56 ? lane : 55;
           const float* src = ok ? img + ((size_t)c * 224 + 2 * sr + dy) * 224 + l * 4 : a.x;
-          glds16_stem(src, slot + j * 1024);
+          glds16_asm(src, slot + j * 1024);
         }
       }
     };
@@ -170,7 +157,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
     // -1 (pool padding).  Half 1's H[6], H[7] and half 0's beyond m=7 are unused.
     auto hpool = [&](v16i c, int (&H)[8]) {
       unsigned x0 = (unsigned)c[0], c16 = (unsigned)c[0];
-      swap32s(x0, c16);  // lanes 0-31: c16 = lanes 32-63's c[0]
+      swap32(x0, c16);  // lanes 0-31: c16 = lanes 32-63's c[0]
       const int c0v = (q == 0 && lh == 0) ? kIntMin : c[0];
       H[0] = max3i(c0v, c[1], c[2]);
 #pragma unroll

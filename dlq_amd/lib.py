@@ -43,6 +43,9 @@ _SIGS = {
     "dlq_quantize_nchw_to_nhwc_s8": ([_vp, _i, _i, _i, _i, _i, _f, _vp, _vp], _i),
     "dlq_quantize_rows_s8": ([_vp, _i, _i, _i, _f, _vp, _vp], _i),
     "dlq_conv2d_nhwc_s8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp], _i),
+    "dlq_downsample_packed_bytes": ([_i, _i], _sz),
+    "dlq_pack_downsample_weights_s8": ([_vp, _i, _i, _i, _vp], _i),
+    "dlq_conv2d_s2_ds_nhwc_s8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "dlq_stem_packed_bytes": ([], _sz),
     "dlq_pack_stem_weights_s8": ([_vp, _vp, _vp, _vp], _i),
     "dlq_stem_fused_s8": ([_vp, _i, _vp, _vp, _vp, _f, _vp, _vp], _i),

@@ -87,6 +87,18 @@ def pack_stem_weights(q_oihw: np.ndarray, alpha: np.ndarray):
     return out, al_out
 
 
+def pack_downsample_weights(q_oc_ic: np.ndarray, C_store: int) -> np.ndarray:
+    """1x1 downsample weights q[OC][IC] for conv2d_s2_ds_nhwc_s8."""
+    q = np.ascontiguousarray(q_oc_ic, np.int8).reshape(q_oc_ic.shape[0], -1)
+    OC, IC = q.shape
+    nb = lib.dlq_downsample_packed_bytes(OC, C_store)
+    if nb == 0:
+        raise ValueError(f"unsupported downsample packing: C={C_store}")
+    out = np.empty(nb, np.int8)
+    check(lib.dlq_pack_downsample_weights_s8(ptr(q), OC, IC, C_store, ptr(out)), "pack_downsample_weights")
+    return out
+
+
 def pad_vec(v, n):
     out = np.zeros(n, np.float32)
     out[: len(v)] = v
@@ -151,6 +163,22 @@ def stem_fused_s8(x: torch.Tensor, w_stem: torch.Tensor, alpha: torch.Tensor, be
     check(lib.dlq_stem_fused_s8(ptr(x), N, ptr(w_stem), ptr(alpha), ptr(beta), inv, ptr(y), stream_handle()),
           "stem_fused_s8")
     return y
+
+
+def conv2d_s2_ds_nhwc_s8(x: torch.Tensor, w_packed: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor,
+                         w_ds: torch.Tensor, alpha_ds: torch.Tensor, beta_ds: torch.Tensor):
+    """3x3/s2 conv (+BN+ReLU) and the fused 1x1/s2 downsample (+BN) of the same
+    NHWC input: returns (y, y_ds), both int8 [N, H/2, W/2, 2C]."""
+    _dev(x, torch.int8)
+    N, H, W, Cc = x.shape
+    OC = 2 * Cc
+    y = torch.empty((N, H // 2, W // 2, OC), dtype=torch.int8, device=x.device)
+    y_ds = torch.empty_like(y)
+    d = ConvDesc(N, H, W, Cc, OC, 3, 3, 2, 2, 1, 1)
+    check(lib.dlq_conv2d_s2_ds_nhwc_s8(C.byref(d), ptr(x), ptr(w_packed), ptr(alpha), ptr(beta), ptr(w_ds),
+                                       ptr(alpha_ds), ptr(beta_ds), ptr(y), ptr(y_ds), stream_handle()),
+          "conv2d_s2_ds_nhwc_s8")
+    return y, y_ds
 
 
 def linear_s8(x: torch.Tensor, w_packed: torch.Tensor, OC: int, alpha=None, beta=None,

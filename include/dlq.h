@@ -86,7 +86,8 @@ typedef struct dlq_conv_desc {
  * Supported: C % 64 == 0 (any kH, kW), the stem (C == 4, 7x7), and C % 32 ==
  * 0 for the wide stride-1 3x3 convs.  Returns 0 for unsupported shapes.
  * Layouts (q = OIHW int8):
- *  - wide stride-1 3x3 (C == OC in {128 @28x28, 256 @14x14, 512 @7x7}, s1 p1):
+ *  - wide 3x3: stride 1 (C == OC in {128 @28x28, 256 @14x14, 512 @7x7}, p1)
+ *    and stride 2 (C -> 2C at 56x56x64, 28x28x128, 14x14x256, p1):
  *      [OCp/128][C/32][128 oc][9 taps x 32 channels + 16 zero bytes]
  *    one contiguous 38,912-byte block per (128-oc tile, 32-channel slice),
  *    copied verbatim into LDS (row pitch 304 B: conflict-free ds_read_b128);
@@ -126,6 +127,21 @@ int dlq_quantize_rows_s8(const float* x, int rows, int cols, int ldy, float inv_
 int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
                        const float* alpha, const float* beta, const int8_t* residual,
                        float res_scale, int relu, int out_kind, void* y, void* stream);
+
+/* Downsampling BasicBlock front (infer_e2e.cu:161-176 conv1 + bn + relu and
+ * :187-196 the 1x1/s2 downsample conv + bn) in one launch: the 3x3/s2/p1
+ * conv (C -> 2C; weights packed by dlq_pack_conv_weights_s8 for `d`) ->
+ * alpha/beta -> ReLU -> int8 y, and the 1x1/s2 conv of the same input
+ * (weights q_ds[OC][IC] packed by dlq_pack_downsample_weights_s8 as
+ * [OCp/128][C/32][128][32 + 16 zero]) -> alpha_ds/beta_ds -> int8 y_ds (no
+ * ReLU).  Both in output-grid units (dlq_fold_bn).  Supported for the
+ * ResNet-18 shapes 56x56x64, 28x28x128 and 14x14x256 (NHWC input).  Results
+ * equal two dlq_conv2d_nhwc_s8 calls (3x3/s2 with relu, 1x1/s2 without). */
+size_t dlq_downsample_packed_bytes(int OC, int C);
+int dlq_pack_downsample_weights_s8(const int8_t* q_ds, int OC, int IC, int C, int8_t* packed);
+int dlq_conv2d_s2_ds_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
+                             const float* alpha, const float* beta, const int8_t* w_ds, const float* alpha_ds,
+                             const float* beta_ds, int8_t* y, int8_t* y_ds, void* stream);
 
 /* Fused stem: fp32 NCHW x[N][3][224][224] -> int8 NHWC y[N][56][56][64] =
  * maxpool3x3s2p1(requant(ReLU(BN(conv7x7s2p3(quant(x)))))).  One launch

@@ -73,6 +73,8 @@ def test_conv_fused_epilogue_bitexact(gpu, shape, residual):
     name, IC, OC, k, s, p, H = shape
     if residual and IC == 3:
         pytest.skip("the stem has no residual input")
+    if residual and k == 3 and s == 2:
+        pytest.skip("a stride-2 conv1 has no residual input (the API rejects one, see test_errors)")
     rng = np.random.default_rng(7 + sum(map(ord, name)))
     N = 2
     x = rand_s8(rng, (N, IC, H, H))
@@ -116,6 +118,32 @@ def test_stem_fused_bitexact(gpu, N):
     y = ops.stem_fused_s8(_cuda(x), _cuda(wst), _cuda(al_p), _cuda(beta), s_in)
     got = nhwc_to_nchw(y.cpu().numpy())
     assert np.array_equal(got, ref), f"{np.count_nonzero(got != ref)} int8 mismatches"
+
+
+@pytest.mark.parametrize("C,H,N", [(64, 56, 3), (128, 28, 5), (256, 14, 37)])
+def test_s2_conv_with_fused_downsample_bitexact(gpu, C, H, N):
+    """layerX.0: 3x3/s2 conv1 (+BN+ReLU) and the 1x1/s2 downsample (+BN, no
+    ReLU) from ONE launch == the oracle's two convs (infer_e2e.cu:161-196)."""
+    from dlq_amd import ops
+    rng = np.random.default_rng(C * 7 + N)
+    OC = 2 * C
+    x = rand_s8(rng, (N, C, H, H))
+    w, bn = rand_conv(rng, OC, C, 3)
+    wd, bnd = rand_conv(rng, OC, C, 1)
+    bnd[0][::5] *= -1
+    wq, sw = O.quantize_weights_s8(w)
+    wdq, swd = O.quantize_weights_s8(wd)
+    s_x, s_y, s_d = 0.03, 0.045, 0.06
+    alpha, beta = O.fold_bn(s_x, sw, bn, s_y)
+    alpha_d, beta_d = O.fold_bn(s_x, swd, bnd, s_d)
+    ref = O.epilogue_s8(O.conv_s8_acc(x, wq, 2, 1), alpha, beta, None, 0.0, True)
+    ref_d = O.epilogue_s8(O.conv_s8_acc(x, wdq, 2, 0), alpha_d, beta_d, None, 0.0, False)
+    xd, wdev = _gpu_conv_inputs(x, wq, 2, 1)
+    wds = _cuda(ops.pack_downsample_weights(wdq.reshape(OC, C), C))
+    y, y_ds = ops.conv2d_s2_ds_nhwc_s8(xd, wdev, _cuda(alpha), _cuda(beta), wds, _cuda(alpha_d), _cuda(beta_d))
+    got, got_d = nhwc_to_nchw(y.cpu().numpy()), nhwc_to_nchw(y_ds.cpu().numpy())
+    assert np.array_equal(got, ref), f"conv1: {np.count_nonzero(got != ref)} mismatches"
+    assert np.array_equal(got_d, ref_d), f"downsample: {np.count_nonzero(got_d != ref_d)} mismatches"
 
 
 @pytest.mark.parametrize("C,H,N", [(128, 28, 90), (256, 14, 180), (512, 7, 360)])
