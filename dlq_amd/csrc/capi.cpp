@@ -295,8 +295,16 @@ int dlq_stem_fused_s8(const float* x, int N, const int8_t* w_stem, const float* 
 int dlq_linear_s8(const int8_t* x, int N, int K, const int8_t* w_packed, int OC, const float* alpha,
                   const float* beta, int relu, int out_kind, void* y, void* stream) {
   if (K <= 0 || K % 64) return fail(DLQ_ERR_ARG, "linear: K must be a positive multiple of 64");
-  dlq_conv_desc d{N, 1, 1, K, OC, 1, 1, 1, 1, 0, 0};
-  return dlq_conv2d_nhwc_s8(&d, x, w_packed, alpha, beta, nullptr, 0.f, relu, out_kind, y, stream);
+  if (N < 0 || OC <= 0) return fail(DLQ_ERR_ARG, "linear: bad shape");
+  if (out_kind < 0 || out_kind > 2) return fail(DLQ_ERR_ARG, "linear: bad out_kind");
+  if (N == 0) return DLQ_OK;
+  if (!x || !w_packed || !y) return fail(DLQ_ERR_ARG, "linear: null pointer");
+  if (out_kind != DLQ_OUT_S32 && (!alpha || !beta)) return fail(DLQ_ERR_ARG, "linear: alpha/beta required");
+  if (out_kind == DLQ_OUT_S8 && OC % 4) return fail(DLQ_ERR_ARG, "linear: int8 output needs OC % 4 == 0");
+  if ((long long)N * K >= (1LL << 31) || (long long)N * OC * 4 >= (1LL << 31))
+    return fail(DLQ_ERR_ARG, "linear: tensor exceeds 2^31 bytes; split the batch");
+  hipError_t e = launch_linear(x, N, K, w_packed, OC, alpha, beta, relu, out_kind, y, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("linear launch: ") + hipGetErrorString(e));
 }
 
 int dlq_maxpool2d_3x3_s2p1_nhwc_s8(const int8_t* x, int N, int C, int H, int W, int8_t* y,
@@ -311,7 +319,8 @@ int dlq_maxpool2d_3x3_s2p1_nhwc_s8(const int8_t* x, int N, int C, int H, int W, 
 int dlq_gap_nhwc_s8(const int8_t* x, int N, int C, int HW, float k, int8_t* y, void* stream) {
   if (!x || !y || N < 0 || C <= 0 || C % 4 || HW <= 0) return fail(DLQ_ERR_ARG, "gap: bad args (C % 4 == 0)");
   if (N == 0) return DLQ_OK;
-  hipError_t e = launch_gap(x, N, C, HW, k, y, (hipStream_t)stream);
+  hipError_t e = C % 16 == 0 ? launch_gap(x, N, C, HW, k, y, (hipStream_t)stream)
+                              : launch_gap4(x, N, C, HW, k, y, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, hipGetErrorString(e));
 }
 

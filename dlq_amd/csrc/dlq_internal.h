@@ -62,7 +62,10 @@ hipError_t launch_quantize_nchw_to_nhwc(const float* x, int N, int C, int H, int
 hipError_t launch_quantize_rows(const float* x, int rows, int cols, int ldy, float inv_s,
                                 int8_t* y, hipStream_t s);
 hipError_t launch_maxpool(const int8_t* x, int N, int C, int H, int W, int8_t* y, hipStream_t s);
-hipError_t launch_gap(const int8_t* x, int N, int C, int HW, float k, int8_t* y, hipStream_t s);
+hipError_t launch_gap(const int8_t* x, int N, int C, int HW, float k, int8_t* y, hipStream_t s);   // C % 16 == 0
+hipError_t launch_gap4(const int8_t* x, int N, int C, int HW, float k, int8_t* y, hipStream_t s);  // C % 4 == 0
+hipError_t launch_linear(const int8_t* x, int N, int K, const int8_t* w, int OC, const float* alpha,
+                         const float* beta, int relu, int out_kind, void* y, hipStream_t s);
 hipError_t launch_im2col_nchw(const int8_t* x, int N, int C, int H, int W, int kH, int kW, int sH,
                               int sW, int pH, int pW, int8_t* col, hipStream_t s);
 

@@ -450,7 +450,8 @@ hipError_t launch_maxpool(const int8_t* x, int N, int C, int H, int W, int8_t* y
   return hipGetLastError();
 }
 
-hipError_t launch_gap(const int8_t* x, int N, int C, int HW, float k, int8_t* y, hipStream_t s) {
+// launch_gap (C % 16 == 0) lives in head.hip; this is the any-C fallback.
+hipError_t launch_gap4(const int8_t* x, int N, int C, int HW, float k, int8_t* y, hipStream_t s) {
   const long total = (long)N * (C / 4);
   hipLaunchKernelGGL(gap_nhwc_s8_kernel, dim3(grid_for(total)), dim3(256), 0, s, x, N, C, HW, k,
                      y);
