@@ -285,11 +285,13 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
         }
         const int bu = tap % 3;
         if constexpr (decltype(mfma_on)::value) {
+          if constexpr ((XB & 32) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int fm = 0; fm < WFM; ++fm)
 #pragma unroll
             for (int fn = 0; fn < WFN; ++fn)
               acc[fm][fn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu][fm], fb[bu][fn], acc[fm][fn], 0, 0, 0);
+          if constexpr ((XB & 32) != 0) __builtin_amdgcn_s_setprio(0);
         } else {
 #pragma unroll
           for (int fm = 0; fm < WFM; ++fm) asm volatile("" ::"v"(fa[bu][fm]));

@@ -450,6 +450,20 @@ int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
   return DLQ_OK;
 }
 
+int dlq_basic_block_s8(dlq_resnet18* m, int block, const int8_t* x, int N, int8_t* y, void* stream) {
+  if (!m) return fail(DLQ_ERR_ARG, "basic_block: null model");
+  if (!m->prepared) return fail(DLQ_ERR_STATE, "basic_block: call dlq_resnet18_prepare first");
+  if (block < 0 || block >= (int)m->blocks.size()) return fail(DLQ_ERR_ARG, "basic_block: block index out of range");
+  if (N < 0 || N > m->max_batch) return fail(DLQ_ERR_ARG, "basic_block: batch exceeds prepared max_batch");
+  if (N == 0) return DLQ_OK;
+  if (!x || !y) return fail(DLQ_ERR_ARG, "basic_block: null pointer");
+  const Block& b = m->blocks[block];
+  const int H = m->convs[b.c1].H;
+  int OH, OW;
+  // intermediates in two of the engine's activation buffers (not re-entrant with forward)
+  return basic_block_forward(m, b, x, N, H, H, m->buf[2], m->buf[3], y, (hipStream_t)stream, &OH, &OW);
+}
+
 int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, void* stream) {
   if (!m) return fail(DLQ_ERR_ARG, "forward: null model");
   if (!m->prepared) return fail(DLQ_ERR_STATE, "forward: call dlq_resnet18_prepare first");

@@ -43,6 +43,20 @@ _SIGS = {
     "dlq_quantize_nchw_to_nhwc_s8": ([_vp, _i, _i, _i, _i, _i, _f, _vp, _vp], _i),
     "dlq_quantize_rows_s8": ([_vp, _i, _i, _i, _f, _vp, _vp], _i),
     "dlq_conv2d_nhwc_s8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp], _i),
+    "dlq_init": ([_i], _i),
+    "dlq_finalize": ([], _i),
+    "dlq_quantize_f32_s8": ([_vp, _sz, _f, _vp, _vp], _i),
+    "dlq_gemm_s8s8s32": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
+    "dlq_conv2d_nchw_workspace_bytes": ([_i] * 11, _sz),
+    "dlq_conv2d_nchw_s8": ([_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp,
+                            _sz, _vp, C.POINTER(_i), C.POINTER(_i)], _i),
+    "dlq_bn_relu_requant_s8": ([_vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp], _i),
+    "dlq_add_relu_requant_s8": ([_vp, _vp, _sz, _f, _f, _i, _vp, _vp], _i),
+    "dlq_maxpool2d_3x3_s2p1_nchw_s8": ([_vp, _i, _i, _i, _i, _vp, _vp], _i),
+    "dlq_gap_s8": ([_vp, _i, _i, _i, _f, _vp, _vp], _i),
+    "dlq_fc_s8": ([_vp, _i, _i, _vp, _i, _vp, _vp, _vp, _vp], _i),
+    "dlq_dequant_s32_f32": ([_vp, _i, _i, _i, _vp, _vp, _vp], _i),
+    "dlq_basic_block_s8": ([_vp, _i, _vp, _i, _vp, _vp], _i),
     "dlq_downsample_packed_bytes": ([_i, _i], _sz),
     "dlq_pack_downsample_weights_s8": ([_vp, _i, _i, _i, _vp], _i),
     "dlq_conv2d_s2_ds_nhwc_s8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),

@@ -100,6 +100,59 @@ size_t dlq_conv_packed_bytes(const dlq_conv_desc* d);
 int dlq_pack_conv_weights_s8(const dlq_conv_desc* d, const int8_t* q_oihw, int IC, int8_t* packed);
 
 /* ------------------------------------------------------------------------ */
+/* Per-layer C-ABI in the reference's layout (layerops.hip).  These mirror   */
+/* the reference's extern "C" kernels and host helpers (RK/include/          */
+/* utils.hpp:74-82, RK/runtime/infer_e2e.cu:64-219): same argument order,    */
+/* NCHW / OIHW / row-major operands, batch honoured, explicit stream, int    */
+/* status.  The NHWC operators further below are the fast path.              */
+/* ------------------------------------------------------------------------ */
+
+/* Select the device and check it is gfx950 (the kernels' only target).    */
+int dlq_init(int device);
+/* Synchronise the device; pairs with dlq_init.                            */
+int dlq_finalize(void);
+/* q[i] = clamp(rne(x[i] * inv_s), +-127): the input quantisation (new; the
+ * reference feeds fp32 straight to im2col, RK/runtime/infer_e2e.cu:255-256). */
+int dlq_quantize_f32_s8(const float* x, size_t n, float inv_s, int8_t* q, void* stream);
+/* sgemm_tiled (RK/kernels/sgemm_tiled.cu:5-46) on int8: C[M][N] (int32) =
+ * A[M][K] . B[K][N], all row-major, any M, N, K. */
+int dlq_gemm_s8s8s32(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, void* stream);
+/* conv2d_nchw_im2col_gemm (RK/runtime/infer_e2e.cu:102-136; + bn_launch
+ * :83-97 + relu) on int8: x[N][IC][H][W], w_oihw[OC][IC][kH][kW] (int8,
+ * packed and uploaded per call like the reference's per-call weight copy),
+ * alpha/beta[OCp] (dlq_fold_bn), out_kind DLQ_OUT_S8 (y int8 NCHW) or
+ * DLQ_OUT_S32 (y int32 NCHW accumulators).  *OH, *OW as the reference
+ * returns them.  workspace >= dlq_conv2d_nchw_workspace_bytes(...) device
+ * bytes.  Shapes: those dlq_conv2d_nhwc_s8 supports (IC % 64 == 0, the RGB
+ * stem, the wide 3x3 convs). */
+size_t dlq_conv2d_nchw_workspace_bytes(int N, int IC, int H, int W, int OC, int kH, int kW, int sH, int sW, int pH,
+                                       int pW);
+int dlq_conv2d_nchw_s8(const int8_t* x, int N, int IC, int H, int W, const int8_t* w_oihw, int OC, int kH, int kW,
+                       int sH, int sW, int pH, int pW, const float* alpha, const float* beta, int relu, int out_kind,
+                       void* y, void* workspace, size_t ws_bytes, void* stream, int* OH, int* OW);
+/* bn_inference + relu_forward (RK/kernels/bn_inference.cu:5-28, relu.cu:4-10)
+ * as the standalone requantising epilogue: y = clamp(rne(fma(acc, alpha[c],
+ * beta[c])), relu ? 0 : -127, 127) on NCHW [N][C][HW]. */
+int dlq_bn_relu_requant_s8(const int32_t* acc, int N, int C, int HW, const float* alpha, const float* beta, int relu,
+                           int8_t* y, void* stream);
+/* add_inplace + relu_forward (RK/kernels/add.cu:2-8) in the int8 domain:
+ * y = clamp(rne(fma(r, r_scale, a * a_scale)), relu ? 0 : -127, 127), with
+ * a_scale = s_a/s_y, r_scale = s_r/s_y (output-grid units). */
+int dlq_add_relu_requant_s8(const int8_t* a, const int8_t* r, size_t n, float a_scale, float r_scale, int relu,
+                            int8_t* y, void* stream);
+/* maxpool2d_3x3_s2p1_nchw (RK/kernels/maxpool2d.cu:4-41) on int8 NCHW. */
+int dlq_maxpool2d_3x3_s2p1_nchw_s8(const int8_t* x, int N, int C, int H, int W, int8_t* y, void* stream);
+/* gap_global (RK/kernels/gap_global.cu:2-33) on int8 NCHW [N][C][HW] ->
+ * int8 [N][C]: exact int32 sum, clamp(rne(float(sum) * k)). */
+int dlq_gap_s8(const int8_t* x, int N, int C, int HW, float k, int8_t* y, void* stream);
+/* fc_forward (RK/runtime/infer_e2e.cu:206-219, bias on the device):
+ * logits[N][OC] = fma(acc, alpha, bias) = dlq_linear_s8(..., DLQ_OUT_F32). */
+int dlq_fc_s8(const int8_t* g, int N, int K, const int8_t* w_packed, int OC, const float* alpha, const float* bias,
+              float* logits, void* stream);
+/* y = float(acc) * scale[c] on NCHW [N][C][HW] (int32 -> fp32 dequant). */
+int dlq_dequant_s32_f32(const int32_t* acc, int N, int C, int HW, const float* scale, float* y, void* stream);
+
+/* ------------------------------------------------------------------------ */
 /* Device operators (per-layer entry points; all asynchronous on `stream`)  */
 /* ------------------------------------------------------------------------ */
 
@@ -212,6 +265,11 @@ int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream);
 int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, void* stream);
 /* Keep snapshots of every stage output (for dumps/parity; costs D2D copies
  * inside forward).  Takes effect at the next dlq_resnet18_prepare. */
+/* basic_block_forward (RK/runtime/infer_e2e.cu:139-203) of block 0..7
+ * (layer1.0 .. layer4.1) of a prepared model on int8 NHWC x (scale of the
+ * block input) -> int8 NHWC y (scale of the block's conv2); intermediates
+ * live in the model's workspace (do not overlap with a forward). */
+int dlq_basic_block_s8(dlq_resnet18* m, int block, const int8_t* x, int N, int8_t* y, void* stream);
 int dlq_resnet18_set_keep_stages(dlq_resnet18* m, int on);
 /* Copy a stage activation of the last forward to device memory `dst`:
  * "input_q", "conv1", "stem_pool", "layer1".."layer4" (int8 NHWC) or

@@ -292,6 +292,19 @@ ORA_API void ora_epilogue_s8(const int32_t* acc, int N, int OC, int HW, const fl
       }
 }
 
+/* add_inplace (RK/kernels/add.cu:7) + relu in the int8 domain:
+ * y = clamp(rne(fmaf(r, r_s, a * a_s)), relu ? 0 : -127, 127). */
+ORA_API void ora_add_requant_s8(const int8_t* a, const int8_t* r, size_t n, float a_s, float r_s, int relu,
+                                int8_t* out) {
+  const float lo = relu ? 0.f : -127.f;
+  for (size_t i = 0; i < n; ++i) {
+    float y = fmaf((float)r[i], r_s, (float)a[i] * a_s);
+    y = y < lo ? lo : y;
+    y = y > 127.f ? 127.f : y;
+    out[i] = (int8_t)(int)rintf(y);
+  }
+}
+
 /* fp32 epilogue (FC logits / dequant): y = fmaf(float(acc), alpha, beta). */
 ORA_API void ora_epilogue_f32(const int32_t* acc, int N, int OC, int HW, const float* alpha,
                               const float* beta, int relu, float* out) {

@@ -46,6 +46,7 @@ _SIGS = {
     "ora_conv2d_nchw_s8_acc": [_s8p, _i, _i, _i, _i, _s8p, _i, _i, _i, _i, _i, _i, _i, _s32p],
     "ora_epilogue_s8": [_s32p, _i, _i, _i, _f32p, _f32p, C.c_void_p, _f, _i, _s8p],
     "ora_epilogue_f32": [_s32p, _i, _i, _i, _f32p, _f32p, _i, _f32p],
+    "ora_add_requant_s8": [_s8p, _s8p, C.c_size_t, _f, _f, _i, _s8p],
     "ora_maxpool_s8": [_s8p, _i, _i, _i, _i, _s8p],
     "ora_gap_s8": [_s8p, _i, _i, _i, _f, C.c_void_p, _s8p],
     "ora_fc_s8": [_s8p, _i, _i, _s8p, _i, _f32p, _f32p, C.c_void_p, _f32p],
@@ -233,6 +234,13 @@ def epilogue_s8(acc, alpha, beta, res=None, r_s=0.0, relu=True):
     r = None if res is None else _c(res, np.int8)
     lib().ora_epilogue_s8(_c(acc, np.int32), N, OC, HW, _c(alpha, np.float32), _c(beta, np.float32),
                           _ptr(r), np.float32(r_s), int(relu), out)
+    return out
+
+
+def add_requant_s8(a, r, a_s, r_s, relu=True):
+    a = _c(a, np.int8); r = _c(r, np.int8)
+    out = np.empty(a.shape, np.int8)
+    lib().ora_add_requant_s8(a, r, a.size, np.float32(a_s), np.float32(r_s), int(relu), out)
     return out
 
 

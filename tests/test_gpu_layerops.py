@@ -1,0 +1,179 @@
+"""GPU parity of the per-layer C-ABI in the reference's layout (NCHW / OIHW /
+row-major, layerops.hip) against the CPU oracle."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests.helpers import model_and_scales, nchw_to_nhwc, nhwc_to_nchw, rand_conv, rand_s8
+
+pytestmark = pytest.mark.gpu
+
+
+def _cuda(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+_KEEP = []  # device copies stay alive until the test's calls are done (a temporary's memory can be reused)
+
+
+def _p(t):
+    _KEEP.append(t)
+    return C.c_void_p(t.data_ptr())
+
+
+@pytest.fixture(autouse=True)
+def _release():
+    yield
+    torch.cuda.synchronize()
+    _KEEP.clear()
+
+
+def _ok(rc):
+    from dlq_amd.lib import lib
+    assert rc == 0, lib.dlq_last_error()
+
+
+def test_init_finalize(gpu):
+    from dlq_amd.lib import lib
+    _ok(lib.dlq_init(0))
+    _ok(lib.dlq_finalize())
+
+
+def test_quantize_f32_s8(gpu):
+    from dlq_amd.lib import lib
+    rng = np.random.default_rng(1)
+    x = (rng.standard_normal(100003, dtype=np.float32) * 3).astype(np.float32)
+    x[:6] = [0.5, 1.5, -2.5, 1e9, -1e9, 0.0]
+    s = np.float32(0.021)
+    q = torch.empty(x.size, dtype=torch.int8, device="cuda")
+    _ok(lib.dlq_quantize_f32_s8(_p(_cuda(x)), x.size, float(O.inv_scale(s)), _p(q), None))
+    torch.cuda.synchronize()
+    assert np.array_equal(q.cpu().numpy(), O.quantize_f32_s8(x, s))
+
+
+@pytest.mark.parametrize("M,N,K", [(100, 77, 61), (1000, 1, 512), (64, 3136, 576), (33, 65, 1)])
+def test_gemm_s8s8s32_reference_layout(gpu, M, N, K):
+    from dlq_amd.lib import lib
+    rng = np.random.default_rng(M + N + K)
+    A = rand_s8(rng, (M, K))
+    B = rand_s8(rng, (K, N))
+    ref = np.empty((M, N), np.int32)
+    O.lib().ora_gemm_s8s8s32(A, B, ref, M, N, K)
+    Cd = torch.empty((M, N), dtype=torch.int32, device="cuda")
+    _ok(lib.dlq_gemm_s8s8s32(_p(_cuda(A)), _p(_cuda(B)), _p(Cd), M, N, K, None))
+    torch.cuda.synchronize()
+    assert np.array_equal(Cd.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("IC,OC,k,s,p,H,N", [(3, 64, 7, 2, 3, 224, 1), (64, 64, 3, 1, 1, 56, 2),
+                                             (64, 128, 1, 2, 0, 56, 2), (128, 128, 3, 1, 1, 28, 3),
+                                             (256, 512, 3, 2, 1, 14, 2)])
+@pytest.mark.parametrize("out_kind", [0, 2])
+def test_conv2d_nchw_reference_signature(gpu, IC, OC, k, s, p, H, N, out_kind):
+    """conv2d_nchw_im2col_gemm's argument order (infer_e2e.cu:102-107): NCHW
+    in/out, OIHW weights, (OH, OW) returned."""
+    from dlq_amd.lib import lib
+    rng = np.random.default_rng(IC * 3 + OC + k)
+    x = rand_s8(rng, (N, IC, H, H))
+    w, bn = rand_conv(rng, OC, IC, k)
+    wq, sw = O.quantize_weights_s8(w)
+    alpha, beta = O.fold_bn(0.03, sw, bn, 0.05)
+    acc = O.conv_s8_acc(x, wq, s, p)
+    ref = acc if out_kind == 2 else O.epilogue_s8(acc, alpha, beta, None, 0.0, True)
+    ocp = lib.dlq_conv_packed_oc(OC)
+    from dlq_amd.ops import pad_vec
+    ws_n = lib.dlq_conv2d_nchw_workspace_bytes(N, IC, H, H, OC, k, k, s, s, p, p)
+    assert ws_n > 0
+    ws = torch.empty(ws_n, dtype=torch.int8, device="cuda")
+    y = torch.empty(ref.shape, dtype=torch.int32 if out_kind == 2 else torch.int8, device="cuda")
+    oh, ow = C.c_int(), C.c_int()
+    _ok(lib.dlq_conv2d_nchw_s8(_p(_cuda(x)), N, IC, H, H, wq.ctypes.data, OC, k, k, s, s, p, p,
+                               _p(_cuda(pad_vec(alpha, ocp))), _p(_cuda(pad_vec(beta, ocp))), 1, out_kind, _p(y),
+                               _p(ws), ws_n, None, C.byref(oh), C.byref(ow)))
+    torch.cuda.synchronize()
+    assert (oh.value, ow.value) == ref.shape[2:]
+    assert np.array_equal(y.cpu().numpy(), ref)
+
+
+def test_bn_relu_add_requant_dequant(gpu):
+    from dlq_amd.lib import lib
+    rng = np.random.default_rng(5)
+    N, Cc, HW = 3, 64, 49
+    acc = rng.integers(-40000, 40000, size=(N, Cc, HW), dtype=np.int32)
+    alpha = (rng.random(Cc, dtype=np.float32) * 2e-3).astype(np.float32)
+    beta = (rng.standard_normal(Cc, dtype=np.float32) * 3).astype(np.float32)
+    for relu in (0, 1):
+        ref = O.epilogue_s8(acc, alpha, beta, None, 0.0, bool(relu))
+        y = torch.empty((N, Cc, HW), dtype=torch.int8, device="cuda")
+        _ok(lib.dlq_bn_relu_requant_s8(_p(_cuda(acc)), N, Cc, HW, _p(_cuda(alpha)), _p(_cuda(beta)), relu, _p(y), None))
+        torch.cuda.synchronize()
+        assert np.array_equal(y.cpu().numpy(), ref)
+    a = rand_s8(rng, (N, Cc, HW), lo=-127)
+    r = rand_s8(rng, (N, Cc, HW), lo=-127)
+    for relu in (0, 1):
+        ref = O.add_requant_s8(a, r, 0.7, 1.3, bool(relu))
+        y = torch.empty(a.shape, dtype=torch.int8, device="cuda")
+        _ok(lib.dlq_add_relu_requant_s8(_p(_cuda(a)), _p(_cuda(r)), a.size, 0.7, 1.3, relu, _p(y), None))
+        torch.cuda.synchronize()
+        assert np.array_equal(y.cpu().numpy(), ref)
+    scale = (rng.random(Cc, dtype=np.float32) * 1e-2).astype(np.float32)
+    yf = torch.empty(acc.shape, dtype=torch.float32, device="cuda")
+    _ok(lib.dlq_dequant_s32_f32(_p(_cuda(acc)), N, Cc, HW, _p(_cuda(scale)), _p(yf), None))
+    torch.cuda.synchronize()
+    ref = acc.astype(np.float32) * scale[None, :, None]
+    assert np.array_equal(yf.cpu().numpy().view(np.int32), ref.view(np.int32))
+
+
+def test_maxpool_gap_fc_nchw(gpu):
+    from dlq_amd import ops
+    from dlq_amd.lib import lib
+    from tests.helpers import golden
+    rng = np.random.default_rng(6)
+    x = rand_s8(rng, (2, 64, 112, 112), lo=-128)
+    y = torch.empty((2, 64, 56, 56), dtype=torch.int8, device="cuda")
+    _ok(lib.dlq_maxpool2d_3x3_s2p1_nchw_s8(_p(_cuda(x)), 2, 64, 112, 112, _p(y), None))
+    torch.cuda.synchronize()
+    assert np.array_equal(y.cpu().numpy(), O.maxpool_s8(x))
+    x4 = rand_s8(rng, (3, 512, 7, 7))
+    k = O.gap_k(0.05, 49, 0.011)
+    g = torch.empty((3, 512), dtype=torch.int8, device="cuda")
+    _ok(lib.dlq_gap_s8(_p(_cuda(x4)), 3, 512, 49, float(k), _p(g), None))
+    torch.cuda.synchronize()
+    gref, _ = O.gap_s8(x4, k)
+    assert np.array_equal(g.cpu().numpy(), gref)
+    W = golden("fc.weight.bin", (1000, 512))
+    bias = golden("fc.bias.bin")
+    wq, sw = O.quantize_weights_s8(W)
+    alpha = O.fc_alpha(0.02, sw)
+    ref, _ = O.fc_s8(gref, wq, alpha, bias)
+    ocp = ops.packed_oc(1000)
+    out = torch.empty((3, 1000), dtype=torch.float32, device="cuda")
+    _ok(lib.dlq_fc_s8(_p(g), 3, 512, _p(_cuda(ops.pack_linear_weights(wq))), 1000, _p(_cuda(ops.pad_vec(alpha, ocp))),
+                      _p(_cuda(ops.pad_vec(bias, ocp))), _p(out), None))
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.int32), ref.view(np.int32))
+
+
+def test_basic_block_api_matches_oracle_stages(gpu):
+    """dlq_basic_block_s8 on blocks 0..3 (layer1.0 .. layer2.1, incl. the
+    fused stride-2 + downsample block) reproduces the oracle's stage dumps."""
+    from dlq_amd.lib import lib
+    from dlq_amd.models import ResNet18Int8, synthetic_images
+    sd, scales = model_and_scales()
+    x = synthetic_images(2, seed=5).numpy()
+    _, dumps = O.resnet18_forward_s8(sd, scales, x)
+    model = ResNet18Int8(sd, scales, max_batch=4)
+    h = model.h
+    cur = _cuda(nchw_to_nhwc(dumps["stem_pool"]))
+    outs = []
+    for b, (Hh, Cc) in enumerate([(56, 64), (56, 64), (28, 128), (28, 128)]):
+        y = torch.empty((2, Hh, Hh, Cc), dtype=torch.int8, device="cuda")
+        _ok(lib.dlq_basic_block_s8(h, b, _p(cur), 2, _p(y), None))
+        cur = y
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert np.array_equal(nhwc_to_nchw(outs[1].cpu().numpy()), dumps["layer1"])
+    assert np.array_equal(nhwc_to_nchw(outs[3].cpu().numpy()), dumps["layer2"])
