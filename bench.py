@@ -29,6 +29,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--prof-steps", type=int, default=10,
+                    help="forwards of the per-kernel event-timing pass after the timed region")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
     ap.add_argument("--cpu-baseline-images", type=int, default=24,
@@ -62,6 +64,23 @@ def shard_gather(forward, x_local, world, out_global=None):
                                  dtype=logits.dtype, device=logits.device)
     dist.all_gather_into_tensor(out_global, logits)
     return out_global
+
+
+def pmc_traffic(kernel_family):
+    """HBM bytes per launch of a kernel family from the committed rocprofv3 PMC
+    summary (profiles/*pmc_traffic.json, written by tools/pmc_traffic.py:
+    FETCH_SIZE doubled per MI355X_MICROARCH.md + WRITE_SIZE), or None."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          "*pmc_traffic.json")))
+    if not paths:
+        return None
+    try:
+        data = json.load(open(paths[-1]))
+        ent = data.get("families", {}).get(kernel_family)
+        return None if ent is None else ent["hbm_bytes_per_launch"]
+    except Exception:
+        return None
 
 
 def cpu_oracle_baseline(sd, scales, n_images):
@@ -99,6 +118,7 @@ def main():
     args = parse()
     rank, world, local = setup_dist()
     dev = torch.device("cuda", local)
+    from dlq_amd.lib import FAMILIES
     from dlq_amd.models import ResNet18Int8, resnet18_state_dict
     from dlq_amd.quant import calibrate_resnet18
     from dlq_amd.models import synthetic_images
@@ -124,7 +144,6 @@ def main():
     for _ in range(args.warmup):
         shard_gather(fwd, x, world, gathered)
     torch.cuda.synchronize()
-    model.set_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -135,8 +154,14 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    conv_ms, n_fwd, n_launch = model.timing()
+    # Per-kernel roofline pass (after the timed region, same stream and inputs):
+    # hipEvents around every launch, grouped by kernel family.
+    model.set_timing(True)
+    for _ in range(args.prof_steps):
+        fwd(x)
+    fam_ms, fam_n, n_fwd = model.timing()
     model.set_timing(False)
+    fam_macs, fam_bytes = model.family_work()
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -145,12 +170,27 @@ def main():
     images = world * B * args.steps
     value = images / dt
     ms_step = dt * 1000.0 / args.steps
-    # Roofline of the dominant kernel: conv_s8_kernel (all 20 convs + FC),
-    # algorithmic int8 ops per launch-sum / event-measured duration.
-    ops_per_fwd = 2.0 * (conv_macs + fc_macs) * B
-    conv_s = conv_ms / 1e3
-    achieved = ops_per_fwd * n_fwd / conv_s / 1e12 if conv_s > 0 else 0.0
-    whole_net_tops = ops_per_fwd * args.steps * world / dt / 1e12
+    whole_net_tops = 2.0 * (conv_macs + fc_macs) * B * args.steps * world / dt / 1e12
+    families = {}
+    for f, name in enumerate(FAMILIES):
+        if fam_n[f] == 0:
+            continue
+        avg_us = fam_ms[f] * 1e3 / fam_n[f]
+        per_fwd = fam_n[f] / max(n_fwd, 1)
+        ent = {"launches_per_forward": round(per_fwd, 2), "avg_launch_us": round(avg_us, 2),
+               "ms_per_forward": round(fam_ms[f] / max(n_fwd, 1), 4)}
+        if fam_macs[f] > 0:
+            ent["tflops_int8"] = round(2.0 * fam_macs[f] * B / per_fwd / (avg_us * 1e-6) / 1e12, 1)
+        if fam_bytes[f] > 0:
+            ent["act_gb_s"] = round(fam_bytes[f] * B / per_fwd / (avg_us * 1e-6) / 1e9, 1)
+        families[name] = ent
+    # Dominant kernel = the family with the most time per forward (MFMA-bound conv).
+    dom = max(range(len(FAMILIES)), key=lambda f: fam_ms[f])
+    dom_avg_us = fam_ms[dom] * 1e3 / max(fam_n[dom], 1)
+    dom_per_fwd = fam_n[dom] / max(n_fwd, 1)
+    ops_per_launch = 2.0 * fam_macs[dom] * B / max(dom_per_fwd, 1e-9)
+    achieved = ops_per_launch / (dom_avg_us * 1e-6) / 1e12 if dom_avg_us > 0 else 0.0
+    traffic = pmc_traffic(FAMILIES[dom])
 
     out = {
         "metric": "images/sec ResNet-18 int8 batch=256 @1/2/4/8 GPU; int8 GEMM TOPS vs peak",
@@ -170,12 +210,14 @@ def main():
                                "N>1 = configs[3] with RCCL logits all-gather)",
                    "global_batch": world * B, "per_gpu_batch": B,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
-        "roofline": {"bound": "mfma", "kernel": "conv_s8_kernel (20 convs + FC per forward)",
+        "roofline": {"bound": "mfma", "kernel": FAMILIES[dom],
                      "achieved": round(achieved, 1), "peak": round(PEAK_I8_TOPS, 1),
                      "unit": "TFLOP/s", "int8_ops": True,
-                     "frac": round(achieved / PEAK_I8_TOPS, 4), "traffic": None,
-                     "avg_launch_us": round(conv_ms * 1e3 / max(n_launch, 1), 2),
-                     "launches": n_launch},
+                     "frac": round(achieved / PEAK_I8_TOPS, 4), "traffic": traffic,
+                     "ops_per_launch": ops_per_launch, "avg_launch_us": round(dom_avg_us, 2),
+                     "launches_timed": fam_n[dom], "timing": "hipEvents on the forward's stream around "
+                     "every launch, separate pass of prof_steps forwards after the timed region"},
+        "kernels": families,
         "whole_net_tops": round(whole_net_tops, 1),
         "gops_per_image": round(2.0 * (conv_macs + fc_macs) / 1e9, 6),
     }

@@ -78,10 +78,12 @@ struct dlq_resnet18 {
   // optional per-stage copies (parity dumps; infer_e2e.cu maybe_save :243-248)
   bool keep = false;
   std::map<std::string, int8_t*> keepbuf;
-  // optional conv-region timing: per forward 6 hipEvents bracketing
-  // [stem conv] [layer1.0.conv1 .. layer4.1.conv2] [fc]
+  // optional per-launch timing: one hipEvent before every kernel launch
+  // (tagged with the launch's kernel family, DLQ_FAM_*) and one after the
+  // last; launch i's duration = elapsed(ev[i], ev[i+1]) on the forward's stream.
   bool timing = false;
   std::vector<hipEvent_t> ev;
+  std::vector<int> ev_tag;  // family of the launch that follows, -1 = end of forward
   size_t ev_used = 0;
 };
 
@@ -203,9 +205,33 @@ int conv2d_nhwc_s8(const dlq_resnet18* m, const ConvLayer& c, const int8_t* x, i
   return dlq_conv2d_nhwc_s8(&d, x, c.w, c.alpha, c.beta, residual, r_s, relu ? 1 : 0, DLQ_OUT_S8, y, s);
 }
 
+int mark(dlq_resnet18* m, hipStream_t s, int family) {
+  if (!m->timing) return DLQ_OK;
+  if (m->ev_used == m->ev.size()) {
+    if (m->ev.size() >= 32 * 4096) return fail(DLQ_ERR_STATE, "timing: event pool full; call dlq_resnet18_timing");
+    hipEvent_t e;
+    hipError_t he = hipEventCreate(&e);
+    if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
+    m->ev.push_back(e);
+    m->ev_tag.push_back(-1);
+  }
+  m->ev_tag[m->ev_used] = family;
+  hipError_t he = hipEventRecord(m->ev[m->ev_used++], s);
+  return he == hipSuccess ? DLQ_OK : hip_fail(he, "hipEventRecord");
+}
+
+// Kernel family of a conv launch (for the per-launch timing).
+int conv_family(const ConvLayer& c, int H) {
+  if (c.k == 3 && c.s == 1 && conv3x3w_shape(c.Cstore, c.OC, H, H, 3, 3, 1, 1, 1, 1) &&
+      wide_layout(c.Cstore, c.OC, H, H, 3, 3, 1, 1, 1, 1))
+    return DLQ_FAM_WIDE;
+  if (c.k == 3 && c.s == 1 && c.Cstore == 64 && H == 56) return DLQ_FAM_L1;
+  return DLQ_FAM_OTHER;
+}
+
 // basic_block_forward (infer_e2e.cu:156-203): conv-bn-relu, conv-bn,
 // identity | 1x1 downsample-bn, add, relu -- three launches at most.
-int basic_block_forward(const dlq_resnet18* m, const Block& b, const int8_t* in, int N, int H,
+int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N, int H,
                         int W, int8_t* h, int8_t* dsb, int8_t* out, hipStream_t s, int* OH,
                         int* OW) {
   int h1, w1, h2, w2;
@@ -218,6 +244,7 @@ int basic_block_forward(const dlq_resnet18* m, const Block& b, const int8_t* in,
     // conv1 (3x3/s2) and the 1x1/s2 downsample in one launch
     const ConvLayer& ds = m->convs[b.ds];
     dlq_conv_desc d{N, H, W, c1.Cstore, c1.OC, 3, 3, 2, 2, 1, 1};
+    if ((rc = mark(m, s, DLQ_FAM_S2DS))) return rc;
     rc = dlq_conv2d_s2_ds_nhwc_s8(&d, in, c1.w, c1.alpha, c1.beta, ds.wf, ds.alpha, ds.beta, h, dsb, s);
     if (rc) return rc;
     h1 = out_dim(H, 3, 2, 1);
@@ -225,10 +252,12 @@ int basic_block_forward(const dlq_resnet18* m, const Block& b, const int8_t* in,
     skip = dsb;
     s_skip = m->scales.at(ds.site);
   } else {
+    if ((rc = mark(m, s, conv_family(c1, H)))) return rc;
     rc = conv2d_nhwc_s8(m, c1, in, N, H, W, nullptr, 0.f, true, h, s, &h1, &w1);
     if (rc) return rc;
     if (b.down) {
       int hd, wd;
+      if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
       rc = conv2d_nhwc_s8(m, m->convs[b.ds], in, N, H, W, nullptr, 0.f, false, dsb, s, &hd, &wd);
       if (rc) return rc;
       if (hd != h1 || wd != w1) return fail(DLQ_ERR_STATE, "downsample shape mismatch");
@@ -236,6 +265,7 @@ int basic_block_forward(const dlq_resnet18* m, const Block& b, const int8_t* in,
       s_skip = m->scales.at(m->convs[b.ds].site);
     }
   }
+  if ((rc = mark(m, s, conv_family(m->convs[b.c2], h1)))) return rc;
   rc = conv2d_nhwc_s8(m, m->convs[b.c2], h, N, h1, w1, skip, s_skip, true, out, s, &h2, &w2);
   *OH = h2;
   *OW = w2;
@@ -253,19 +283,6 @@ int record_stage(dlq_resnet18* m, const char* name, const int8_t* p, size_t byte
   }
   m->stage[name] = {p, bytes};
   return DLQ_OK;
-}
-
-int mark(dlq_resnet18* m, hipStream_t s) {
-  if (!m->timing) return DLQ_OK;
-  if (m->ev_used == m->ev.size()) {
-    if (m->ev.size() >= 6 * 8192) return fail(DLQ_ERR_STATE, "timing: event pool full; call dlq_resnet18_timing");
-    hipEvent_t e;
-    hipError_t he = hipEventCreate(&e);
-    if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
-    m->ev.push_back(e);
-  }
-  hipError_t he = hipEventRecord(m->ev[m->ev_used++], s);
-  return he == hipSuccess ? DLQ_OK : hip_fail(he, "hipEventRecord");
 }
 
 int check_ready(const dlq_resnet18* m) {
@@ -480,27 +497,26 @@ int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, 
   if (!unfused_stem()) {
     // 0+1) fused stem: quantise + conv 7x7/s2 + BN + ReLU + maxpool 3x3/s2
     //      (infer_e2e.cu:255-293) in one launch
-    if ((rc = mark(m, s))) return rc;
+    if ((rc = mark(m, s, DLQ_FAM_STEM))) return rc;
     rc = dlq_stem_fused_s8(x, B, m->stem_w, m->stem_alpha, st.beta, inv_scale(m->scales.at("input")), cur, stream);
     if (rc) return rc;
-    if ((rc = mark(m, s))) return rc;
   } else {
     // unfused reference sequence (A/B and parity of the fused kernel)
+    if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
     rc = dlq_quantize_nchw_to_nhwc_s8(x, B, 3, 224, 224, kStemC, inv_scale(m->scales.at("input")), m->xq, stream);
     if (rc) return rc;
     m->stage["input_q"] = {m->xq, nB * 224 * 224 * kStemC};
     int CH, CW;
-    if ((rc = mark(m, s))) return rc;
+    if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
     rc = conv2d_nhwc_s8(m, st, m->xq, B, 224, 224, nullptr, 0.f, true, m->c1, s, &CH, &CW);
     if (rc) return rc;
-    if ((rc = mark(m, s))) return rc;
     m->stage["conv1"] = {m->c1, nB * CH * CW * 64};
+    if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
     rc = dlq_maxpool2d_3x3_s2p1_nhwc_s8(m->c1, B, 64, CH, CW, cur, stream);
     if (rc) return rc;
   }
   if ((rc = record_stage(m, "stem_pool", cur, nB * H * W * 64, s))) return rc;
   // 2-5) layer1..layer4 (:300-415)
-  if ((rc = mark(m, s))) return rc;
   for (size_t bi = 0; bi < m->blocks.size(); ++bi) {
     const Block& b = m->blocks[bi];
     int8_t* fr[3];
@@ -516,18 +532,18 @@ int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, 
     if (b.name.size() == 8 && b.name[7] == '1')
       if ((rc = record_stage(m, b.name.substr(0, 6).c_str(), cur, nB * H * W * b.oc, s))) return rc;
   }
-  if ((rc = mark(m, s))) return rc;
   // 6) GAP + FC (:417-433)
   const std::string last = m->convs[m->blocks.back().c2].site;
   const float k = (m->scales.at(last) / (float)(H * W)) / m->scales.at("gap");
+  if ((rc = mark(m, s, DLQ_FAM_GAP))) return rc;
   rc = dlq_gap_nhwc_s8(cur, B, 512, H * W, k, m->gq, stream);
   if (rc) return rc;
   m->stage["gap"] = {m->gq, nB * 512};
-  if ((rc = mark(m, s))) return rc;
+  if ((rc = mark(m, s, DLQ_FAM_FC))) return rc;
   rc = dlq_linear_s8(m->gq, B, 512, m->fc_w, 1000, m->fc_alpha, m->fc_beta, 0, DLQ_OUT_F32,
                      logits, stream);
   if (rc) return rc;
-  if ((rc = mark(m, s))) return rc;
+  if ((rc = mark(m, s, -1))) return rc;
   m->last_B = B;
   return DLQ_OK;
 }
@@ -539,25 +555,59 @@ int dlq_resnet18_set_timing(dlq_resnet18* m, int on) {
   return DLQ_OK;
 }
 
-int dlq_resnet18_timing(dlq_resnet18* m, double* conv_ms, int* forwards, int* conv_launches) {
-  if (!m) return fail(DLQ_ERR_ARG, "timing: null");
-  double total = 0;
-  const size_t n = m->ev_used / 6;
-  for (size_t f = 0; f < n; ++f) {
-    hipEvent_t* e = &m->ev[6 * f];
-    for (int r = 0; r < 3; ++r) {
-      hipError_t he = hipEventSynchronize(e[2 * r + 1]);
-      if (he != hipSuccess) return hip_fail(he, "hipEventSynchronize");
-      float ms = 0;
-      he = hipEventElapsedTime(&ms, e[2 * r], e[2 * r + 1]);
-      if (he != hipSuccess) return hip_fail(he, "hipEventElapsedTime");
-      total += ms;
-    }
+int dlq_resnet18_timing(dlq_resnet18* m, double* ms, int* launches, int* forwards) {
+  if (!m || !ms || !launches) return fail(DLQ_ERR_ARG, "timing: null");
+  for (int f = 0; f < DLQ_FAM_COUNT; ++f) {
+    ms[f] = 0.0;
+    launches[f] = 0;
   }
-  if (conv_ms) *conv_ms = total;
-  if (forwards) *forwards = (int)n;
-  if (conv_launches) *conv_launches = (int)(n * (m->convs.size() + 1));
+  int nf = 0;
+  if (m->ev_used > 0) {
+    hipError_t he = hipEventSynchronize(m->ev[m->ev_used - 1]);
+    if (he != hipSuccess) return hip_fail(he, "hipEventSynchronize");
+  }
+  for (size_t i = 0; i + 1 < m->ev_used; ++i) {
+    const int f = m->ev_tag[i];
+    if (f < 0) continue;  // end of one forward -> start of the next
+    float t = 0;
+    hipError_t he = hipEventElapsedTime(&t, m->ev[i], m->ev[i + 1]);
+    if (he != hipSuccess) return hip_fail(he, "hipEventElapsedTime");
+    ms[f] += t;
+    launches[f] += 1;
+  }
+  for (size_t i = 0; i < m->ev_used; ++i) nf += m->ev_tag[i] < 0;
+  if (forwards) *forwards = nf;
   m->ev_used = 0;
+  return DLQ_OK;
+}
+
+int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes) {
+  if (!m || !macs || !bytes) return fail(DLQ_ERR_ARG, "family_work: null");
+  for (int f = 0; f < DLQ_FAM_COUNT; ++f) macs[f] = bytes[f] = 0.0;
+  // stem: fp32 input read + pooled int8 output written, 7x7x3 MACs at 112x112
+  const ConvLayer& st = m->convs[m->stem];
+  macs[DLQ_FAM_STEM] = (double)st.OC * st.IC * st.k * st.k * 112.0 * 112.0;
+  bytes[DLQ_FAM_STEM] = 3.0 * 224 * 224 * 4 + 56.0 * 56 * 64;
+  for (const Block& b : m->blocks) {
+    const ConvLayer& c1 = m->convs[b.c1];
+    const ConvLayer& c2 = m->convs[b.c2];
+    const int H = c1.H, OH = c2.H;
+    const double mac1 = (double)c1.OC * c1.IC * 9 * OH * OH, mac2 = (double)c2.OC * c2.IC * 9 * OH * OH;
+    const double in1 = (double)H * H * c1.IC, out = (double)OH * OH * c2.OC;
+    if (b.down) {
+      const ConvLayer& ds = m->convs[b.ds];
+      macs[DLQ_FAM_S2DS] += mac1 + (double)ds.OC * ds.IC * OH * OH;
+      bytes[DLQ_FAM_S2DS] += in1 + 2 * out;
+    } else {
+      macs[conv_family(c1, H)] += mac1;
+      bytes[conv_family(c1, H)] += in1 + out;
+    }
+    macs[conv_family(c2, OH)] += mac2;
+    bytes[conv_family(c2, OH)] += out + out + out;  // input, residual, output
+  }
+  macs[DLQ_FAM_FC] = 512.0 * 1000;
+  bytes[DLQ_FAM_FC] = 512.0 + 4000.0;
+  bytes[DLQ_FAM_GAP] = 7.0 * 7 * 512 + 512;
   return DLQ_OK;
 }
 

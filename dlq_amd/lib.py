@@ -19,6 +19,9 @@ LIB_PATH = os.path.join(_HERE, "libdlq.so")
 
 DLQ_OK = 0
 DLQ_OUT_S8, DLQ_OUT_F32, DLQ_OUT_S32 = 0, 1, 2
+# kernel families of dlq_resnet18_timing (include/dlq.h DLQ_FAM_*)
+FAMILIES = ["stem_fused_kernel", "conv3x3s1_kernel (layer1)", "conv3x3s2_kernel (+downsample)",
+            "conv3x3w_kernel (layer2-4 s1)", "gap16_kernel", "linear_kernel (fc)", "other"]
 
 
 class DLQError(RuntimeError):
@@ -78,7 +81,8 @@ _SIGS = {
     "dlq_resnet18_forward": ([_vp, _vp, _i, _vp, _vp], _i),
     "dlq_resnet18_stage": ([_vp, C.c_char_p, _vp, _sz, C.POINTER(_sz), _vp], _i),
     "dlq_resnet18_set_timing": ([_vp, _i], _i),
-    "dlq_resnet18_timing": ([_vp, C.POINTER(C.c_double), C.POINTER(_i), C.POINTER(_i)], _i),
+    "dlq_resnet18_timing": ([_vp, _vp, _vp, C.POINTER(_i)], _i),
+    "dlq_resnet18_family_work": ([_vp, _vp, _vp], _i),
     "dlq_resnet18_macs_per_image": ([_vp, C.POINTER(C.c_double), C.POINTER(C.c_double)], _i),
     "dlq_mlp_create": ([_i, _i, _i, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, C.POINTER(_vp)], _i),
     "dlq_mlp_destroy": ([_vp], None),

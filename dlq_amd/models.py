@@ -185,10 +185,20 @@ class ResNet18Int8:
         self._check(self._lib.dlq_resnet18_set_timing(self.h, int(on)), "set_timing")
 
     def timing(self):
-        """(conv_ms summed, forwards, conv launches) since set_timing/last call."""
-        ms, nf, nl = C.c_double(), C.c_int(), C.c_int()
-        self._check(self._lib.dlq_resnet18_timing(self.h, C.byref(ms), C.byref(nf), C.byref(nl)), "timing")
-        return ms.value, nf.value, nl.value
+        """Per kernel family (lib.FAMILIES): (summed ms, launches), and the
+        forwards covered since set_timing / the last call."""
+        ms = (C.c_double * 7)()
+        nl = (C.c_int * 7)()
+        nf = C.c_int()
+        self._check(self._lib.dlq_resnet18_timing(self.h, ms, nl, C.byref(nf)), "timing")
+        return list(ms), list(nl), nf.value
+
+    def family_work(self):
+        """Per kernel family: (algorithmic MACs, activation bytes) per image and forward."""
+        macs = (C.c_double * 7)()
+        nbytes = (C.c_double * 7)()
+        self._check(self._lib.dlq_resnet18_family_work(self.h, macs, nbytes), "family_work")
+        return list(macs), list(nbytes)
 
     def macs_per_image(self):
         cm, fm = C.c_double(), C.c_double()

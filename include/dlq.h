@@ -276,13 +276,28 @@ int dlq_resnet18_set_keep_stages(dlq_resnet18* m, int on);
  * "gap" (int8 [B][512]).  *bytes receives the size. */
 int dlq_resnet18_stage(dlq_resnet18* m, const char* name, void* dst, size_t cap, size_t* bytes,
                        void* stream);
-/* Conv-kernel timing: with timing on, every forward records hipEvents on its
- * stream around the stem conv, the 19 block convs (layer1.0.conv1 ..
- * layer4.1.conv2, nothing else launched in between) and the FC GEMM.
- * dlq_resnet18_timing synchronises on them, returns the summed milliseconds,
- * the forwards and conv-kernel launches covered, and resets the counters. */
+/* Per-launch kernel timing: with timing on, every forward records one
+ * hipEvent on its stream before each kernel launch (tagged with the launch's
+ * kernel family below) and one after the last, so launch i lasts
+ * elapsed(event i, event i+1).  dlq_resnet18_timing synchronises, fills
+ * ms[DLQ_FAM_COUNT] (summed milliseconds) and launches[DLQ_FAM_COUNT] per
+ * family, the number of forwards covered, and resets.
+ * dlq_resnet18_family_work gives each family's algorithmic MACs and
+ * activation bytes (input + output (+ residual), weights excluded) per image
+ * and forward, the basis of a roofline's "achieved". */
+enum {
+  DLQ_FAM_STEM = 0,  /* stem_fused_kernel: quantise + conv1 + BN/ReLU + maxpool */
+  DLQ_FAM_L1 = 1,    /* conv3x3s1_kernel: layer1 3x3 convs                      */
+  DLQ_FAM_S2DS = 2,  /* conv3x3s2_kernel: layerX.0 conv1 + fused downsample     */
+  DLQ_FAM_WIDE = 3,  /* conv3x3w_kernel: layer2-4 stride-1 3x3 convs            */
+  DLQ_FAM_GAP = 4,   /* gap16_kernel                                            */
+  DLQ_FAM_FC = 5,    /* linear_kernel (FC)                                      */
+  DLQ_FAM_OTHER = 6, /* any unfused fallback launch                             */
+  DLQ_FAM_COUNT = 7
+};
 int dlq_resnet18_set_timing(dlq_resnet18* m, int on);
-int dlq_resnet18_timing(dlq_resnet18* m, double* conv_ms, int* forwards, int* conv_launches);
+int dlq_resnet18_timing(dlq_resnet18* m, double* ms, int* launches, int* forwards);
+int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes);
 /* Algorithmic MACs per image of the 20 convs and of the FC layer. */
 int dlq_resnet18_macs_per_image(const dlq_resnet18* m, double* conv_macs, double* fc_macs);
 
