@@ -1,0 +1,452 @@
+// block_l1.hip -- one layer1 basic block of ResNet-18 (64 channels at 56x56:
+// conv3x3-BN-ReLU, conv3x3-BN, + identity, ReLU) as ONE launch.
+//
+// Replaces, for this shape, the reference's basic_block_forward
+// (RK/runtime/infer_e2e.cu:156-203: two im2col_nchw + sgemm_tiled convs,
+// bn_launch, add_inplace, relu_forward) -- i.e. two conv launches of
+// conv3x3.hip here.  The intermediate activation never leaves the CU, the
+// block input is read from HBM once (plus an L2-hot re-read as the residual),
+// and each intermediate row is computed exactly once.
+//
+// Work decomposition: one workgroup per image (persistent over images
+// b, b+G, ...).  The images of a workgroup form one stream of "global rows"
+// (image j = rows [56j, 56j+56)), walked in phases of 8 rows; in phase g
+// (G = 8g):
+//   conv1 waves (0-3): intermediate rows [G, G+8) from input rows [G-1, G+9)
+//   conv2 waves (4-7): output rows [G-9, G-1) from intermediate rows [G-10, G)
+//   all waves:         LDS-DMA of input rows [G+9, G+17) for phase g+1
+// so conv2 trails conv1 by one phase and nothing waits inside a phase; one
+// barrier per phase.
+//
+// LDS layout: two rings (input, intermediate) of 18 rows + one zero row,
+// each split into four channel planes (plane p = channels 16p .. 16p+15, 16 B
+// per pixel).  A plane row is 64 units of 16 B: units 0 and 57 are zero
+// padding (the conv's left/right zero columns), units 1..56 the pixels.  With
+// 16-byte pixels, 16 consecutive pixels cover all 64 banks, so the pixel
+// fragments need no swizzle, and a tap's address is its row's base plus an
+// immediate offset (16*kw for the column, 2 planes for the second 32
+// channels): the k-loop issues ds_read_b128 with no address arithmetic.
+// Taps in rows outside the image read the zero row.
+//
+// Each wave owns one conv and 32 of its 64 output channels and keeps that
+// weight slice (32 oc x 576 K = 72 VGPRs) and its alpha/beta in registers for
+// the life of the kernel, so the only LDS operand traffic is the pixel
+// fragment.  A job = 32 oc x 64 pixels x 576 K (36 v_mfma_i32_32x32x32_i8 in
+// four independent accumulation chains); per phase 14 conv1 + 14 conv2 jobs,
+// dealt so that each SIMD (waves w and w+4) gets exactly 7.
+//
+// Epilogues (bit-identical to conv3x3.hip / oracle.c): conv1 y =
+// fma(acc, a1, b1) -> ReLU -> rne -> int8 written to the intermediate ring;
+// conv2 y = fma(acc, a2, b2) + s_res * x -> ReLU -> rne -> int8 to HBM.
+#include <cstdlib>
+#include <utility>
+
+#include "device_common.h"
+
+namespace dlq {
+
+__device__ __attribute__((aligned(64))) int8_t g_trash_b[1024];  // sink for stores of pixels past the end
+__device__ __attribute__((aligned(64))) int8_t g_zero_b[64];     // DMA source of the zero padding units
+
+namespace {
+
+#ifdef DLQ_STAMPS
+// timing-probe builds: per-wave cycle totals by section (no VM ops in the loop)
+__device__ unsigned long long g_bstamps[256 * 8 * 128];
+#define BT_DECL unsigned long long bt_acc[6] = {0, 0, 0, 0, 0, 0}, bt_prev = __builtin_amdgcn_s_memtime()
+#define BT(k)                                              \
+  do {                                                     \
+    const unsigned long long bt_now = __builtin_amdgcn_s_memtime(); \
+    bt_acc[k] += bt_now - bt_prev;                         \
+    bt_prev = bt_now;                                      \
+  } while (0)
+#define BT_STORE()                                                                                 \
+  do {                                                                                             \
+    if ((threadIdx.x & 63) == 0)                                                                   \
+      for (int q_ = 0; q_ < 6; ++q_) g_bstamps[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 128 + q_] = bt_acc[q_]; \
+  } while (0)
+#else
+#define BT_DECL
+#define BT(k) \
+  do {        \
+  } while (0)
+#define BT_STORE() \
+  do {             \
+  } while (0)
+#endif
+
+#ifndef BL1_TEST
+#define BL1_TEST 0  // timing probe builds only: 1/2 conv2/conv1 waves idle, 7 no residual loads, 8 no stores
+#endif
+
+constexpr int LW = 56;               // image height = width
+constexpr int LC = 64;               // channels
+constexpr int RPH = 8;               // rows per phase
+constexpr int NR = 18;               // ring rows (slot NR = the zero row)
+constexpr int PROW = 1024;           // plane row: 64 units of 16 B (pad, 56 pixels, pad, 6 unused)
+constexpr int PL = (NR + 1) * PROW;  // one channel plane of a ring
+constexpr int RING = 4 * PL;
+constexpr int OFF_IN = 0;
+constexpr int OFF_MID = RING;
+constexpr int LDS_TOTAL = 2 * RING;
+static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
+static_assert(2 * PL + 32 < 65536, "ds_read immediate offset");
+constexpr int KS = 18;  // 9 taps x two 32-channel k-steps
+
+struct BlockArgs {
+  const int8_t* x;   // block input [N][56][56][64]
+  int8_t* y;         // block output, same shape
+  const int8_t* w1;  // generic packed 3x3 weights (64 oc x 9 taps x 64 B, chunk-swizzled)
+  const int8_t* w2;
+  const float* a1;
+  const float* b1;
+  const float* a2;
+  const float* b2;
+  float s_res;  // residual scale in conv2's output-grid units
+  int N;
+};
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int pos_mod(int v, int m) { return ((v % m) + m) % m; }
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// ds_read_b128 (register address + immediate offset) the compiler does not
+// track: completion only via wait_lgkm_tie, which also orders the register's
+// later uses after the wait -- so hipcc can neither sink a prefetch next to
+// its use nor collapse the fragment rotation.
+template <int OFF>
+__device__ __forceinline__ v4i ds_read16(unsigned addr) {
+  v4i r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF) : "memory");
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void wait_lgkm_tie(v4i& x, v4i& y) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(x), "+v"(y) : "n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_tie(v4i& x, v4i& y) {
+  asm volatile("s_waitcnt vmcnt(%2)" : "+v"(x), "+v"(y) : "n"(N) : "memory");
+}
+
+__global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
+  __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: roles branch on SGPRs
+  const int lr = lane & 31, lh = lane >> 5;
+  const bool second = wave >= 4;  // conv2 wave
+  const int NG = gridDim.x, b = blockIdx.x;
+  const int J = (a.N - b + NG - 1) / NG;  // images b, b+NG, ... of this workgroup
+  const int rows = J * LW;
+  const int nphase = rows / RPH + 2;  // conv2 trails conv1 by 9 rows
+  const unsigned lds32 = lds_addr32(lds);
+
+  // Zero the intermediate ring (its padding units and zero row are never
+  // written again) and the input ring's zero row.
+  for (int i = tid; i < RING / 16; i += 512) *(v4i*)(lds + OFF_MID + 16 * i) = v4i{0, 0, 0, 0};
+  for (int i = tid; i < 4 * PROW / 16; i += 512)
+    *(v4i*)(lds + OFF_IN + (i >> 6) * PL + NR * PROW + 16 * (i & 63)) = v4i{0, 0, 0, 0};
+
+  // Wave roles: conv (second), output-channel half h (oc h*32 .. h*32+31) and
+  // job parity.  Per phase each conv has 7 jobs of 64 pixels per half; conv1
+  // waves 0,1 take jobs 0,2,4,6 and waves 2,3 jobs 1,3,5; conv2 waves 4,5 take
+  // 1,3,5 and 6,7 take 0,2,4,6 -- so the two waves of every SIMD (w, w+4)
+  // share exactly 7 jobs.
+  const int h = wave & 1, j0 = second ? 1 - ((wave >> 1) & 1) : (wave >> 1) & 1;
+
+  // This wave's weights, resident in VGPRs: wr[ks] = A fragment of k-step ks
+  // (tap ks/2, channels 32*(ks&1) + 16*lh ..) for output channel h*32 + lr.
+  v4i wr[KS];
+  const int8_t* ws = second ? a.w2 : a.w1;
+  const int ol = h * 32 + lr;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int tap = ks >> 1, kk = ks & 1;
+    wr[ks] = *(const v4i*)(ws + ol * 576 + tap * 64 + (((2 * kk + lh) ^ ((ol >> 2) & 3)) << 4));
+  }
+  // alpha/beta of this lane's 16 channels in the MFMA layout (oc h*32 + 8g + 4lh + e)
+  float al[16], be[16];
+  {
+    const float* pa = second ? a.a2 : a.a1;
+    const float* pb = second ? a.b2 : a.b1;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        al[4 * g4 + e] = pa[h * 32 + 8 * g4 + 4 * lh + e];
+        be[4 * g4 + e] = pb[h * 32 + 8 * g4 + 4 * lh + e];
+      }
+  }
+
+  // LDS-DMA of input row R into its ring slot: one piece per (row, plane),
+  // lane i -> unit i of the plane row (pixel i-1; units 0 and 57..63 and rows
+  // outside [0, rows) read zeros).  The row pointer and slot are wave-uniform
+  // (SALU); per lane only the column/plane offset is added.
+  auto row_src = [&](int R) -> const int8_t* {
+    if (R < 0 || R >= rows) return nullptr;
+    const int j = R / LW, r = R - j * LW;
+    return a.x + ((size_t)(b + j * NG) * LW + r) * (LW * LC);
+  };
+  const bool pix_lane = lane >= 1 && lane <= LW;
+  auto dma_piece = [&](int R, int p) {
+    const int8_t* rp = row_src(R);
+    const int8_t* src = (rp && pix_lane) ? rp + (lane - 1) * LC + p * 16 : g_zero_b + (lane & 3) * 16;
+    glds16_asm(src, lds32 + OFF_IN + p * PL + pos_mod(R, NR) * PROW);
+  };
+
+  for (int P = wave; P < 36; P += 8) dma_piece(P >> 2, P & 3);  // rows 0..8
+  wait_vm0();
+  __syncthreads();
+
+  // Row bases of one lane's pixel: slot s0 holds the row above it (s0 + 1,
+  // s0 + 2 the next two, mod NR); r = its image-local row.  ra[kh] = byte
+  // address of unit `col` (= padded position of column col-1) in plane lh of
+  // that row, or of the zero row.
+  auto row_addrs = [&](int ring, int s0, int r, int col, bool valid, unsigned (&ra)[3]) {
+    int sl = s0;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      if (kh) {
+        ++sl;
+        if (sl == NR) sl = 0;
+      }
+      const bool rok = valid && (kh == 0 ? r > 0 : kh == 2 ? r < LW - 1 : true);
+      ra[kh] = lds32 + ring + lh * PL + (rok ? sl : NR) * PROW + 16 * col;
+    }
+  };
+
+  // One job: 32 oc x 64 pixels (two 32-pixel tiles) x 576 K, one
+  // accumulation chain per tile (a dependent v_mfma_i32_32x32x32_i8 chain
+  // issues at the full rate); pixel fragments are read two k-steps ahead.
+  // k-step ks = tap (kh, kw), channel half kk: row base ra[kh], immediate
+  // offset 16*kw + kk*2 planes.
+  auto run_job = [&](const unsigned (&r0)[3], const unsigned (&r1)[3], v16i (&acc)[2]) {
+    acc[0] = v16i{0};
+    acc[1] = v16i{0};
+    v4i bf[3][2];
+    auto ld = [&](auto nc, int buf) {
+      constexpr int n = decltype(nc)::value, tap = n >> 1, kh = tap / 3, kw = tap % 3;
+      constexpr int off = 16 * kw + (n & 1) * 2 * PL;
+      bf[buf][0] = ds_read16<off>(r0[kh]);
+      bf[buf][1] = ds_read16<off>(r1[kh]);
+    };
+    ld(std::integral_constant<int, 0>{}, 0);
+    ld(std::integral_constant<int, 1>{}, 1);
+    auto step = [&](auto kc) {
+      constexpr int ks = decltype(kc)::value;
+      if constexpr (ks + 2 < KS) ld(std::integral_constant<int, ks + 2>{}, (ks + 2) % 3);
+      constexpr int younger = (ks + 2 < KS ? 2 : 0) + (ks + 1 < KS ? 2 : 0);
+      wait_lgkm_tie<younger>(bf[ks % 3][0], bf[ks % 3][1]);
+      acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wr[ks], bf[ks % 3][0], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wr[ks], bf[ks % 3][1], acc[1], 0, 0, 0);
+    };
+    static_for<0, KS>(step);
+  };
+
+  // Epilogue of one 32 oc x 32 px tile in the MFMA layout (lane: pixel lr,
+  // channels h*32 + 8g + 4lh + e) -> 16 contiguous channels (h*32 + 16lh ..)
+  // of the pixel.  rs: the residual's 16 bytes in that store layout (conv2).
+  // Pairs of elements go through v_pk_fma_f32 / v_pk_add_f32 (per-component
+  // IEEE fma / add: bit-identical to the scalar sequence).
+  auto epilogue = [&](const v16i& acc, bool res, v4i rs) -> v4i {
+    unsigned rg[4] = {0, 0, 0, 0};
+    if (res) {  // store layout -> MFMA layout
+      unsigned rr[4] = {(unsigned)rs[0], (unsigned)rs[1], (unsigned)rs[2], (unsigned)rs[3]};
+      swap32(rr[0], rr[1]);
+      swap32(rr[2], rr[3]);
+      rg[0] = rr[0] ^ 0x80808080u;  // biased: int8 v = ubyte(v ^ 0x80) - 128, exact in fp32
+      rg[1] = rr[2] ^ 0x80808080u;
+      rg[2] = rr[1] ^ 0x80808080u;
+      rg[3] = rr[3] ^ 0x80808080u;
+    }
+    const f2 M2 = {12582912.0f, 12582912.0f}, sr2 = {a.s_res, a.s_res}, m128 = {-128.f, -128.f};
+    unsigned qv[4];
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      f2 y[2];
+#pragma unroll
+      for (int p2 = 0; p2 < 2; ++p2) {
+        const int e = 4 * g4 + 2 * p2;
+        y[p2] = __builtin_elementwise_fma(f2{(float)acc[e], (float)acc[e + 1]}, f2{al[e], al[e + 1]},
+                                          f2{be[e], be[e + 1]});
+        if (res) {
+          const f2 rv = f2{(float)((rg[g4] >> (16 * p2)) & 0xffu), (float)((rg[g4] >> (16 * p2 + 8)) & 0xffu)} + m128;
+          y[p2] = __builtin_elementwise_fma(rv, sr2, y[p2]);
+        }
+        y[p2] = f2{__builtin_amdgcn_fmed3f(y[p2][0], 0.f, 127.f), __builtin_amdgcn_fmed3f(y[p2][1], 0.f, 127.f)} + M2;
+      }
+      const unsigned u0 = __float_as_uint(y[0][0]), u1 = __float_as_uint(y[0][1]);
+      const unsigned u2 = __float_as_uint(y[1][0]), u3 = __float_as_uint(y[1][1]);
+      qv[g4] = __builtin_amdgcn_perm(u1, u0, 0x0c0c0400u) | __builtin_amdgcn_perm(u3, u2, 0x04000c0cu);
+    }
+    return mfma_to_store16(qv[0], qv[1], qv[2], qv[3]);
+  };
+
+  // pixel of tile t of job j: phase-relative row ro (0..7) and column
+  auto pix_of = [&](int j, int t, int& ro, int& col) {
+    const int px = j * 64 + t * 32 + lr;
+    ro = (px * 1171) >> 16;  // px / 56 for px < 448
+    col = px - ro * LW;
+  };
+
+  BT_DECL;
+  for (int g = 0; g < nphase; ++g) {
+    const int G = g * RPH;
+    if (!second) {
+      // conv1 waves also stream the next phase's input rows [G+9, G+17): wave
+      // c issues plane c of all 8 rows, two pieces per job, so only conv1
+      // waves ever wait on LDS-DMA.
+      int kp = 0;
+      auto pieces = [&](int n) {
+        for (int e = 0; e < n && kp < 8; ++e, ++kp) dma_piece(G + 9 + kp, wave);
+      };
+      if (G < rows && BL1_TEST != 2) {
+        // slots of rows G-1 (taps) and G (output), image-local row of G
+        const int S_in = pos_mod(G - 1, NR), S_mid = G % NR, r0 = G % LW;
+        for (int j = j0; j < 7; j += 2) {
+          BT(0);
+          pieces(2);
+          BT(5);
+          unsigned ra[2][3], wa[2];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            int ro, col;
+            pix_of(j, t, ro, col);
+            int s0 = S_in + ro;
+            if (s0 >= NR) s0 -= NR;
+            row_addrs(OFF_IN, s0, r0 + ro, col, true, ra[t]);
+            int sm = S_mid + ro;
+            if (sm >= NR) sm -= NR;
+            wa[t] = OFF_MID + (2 * h + lh) * PL + sm * PROW + 16 * (col + 1);
+          }
+          v16i acc[2];
+          BT(0);
+          run_job(ra[0], ra[1], acc);
+          BT(1);
+#pragma unroll
+          for (int t = 0; t < 2; ++t) *(v4i*)(lds + wa[t]) = epilogue(acc[t], false, v4i{0, 0, 0, 0});
+          BT(2);
+        }
+      }
+      if (G + 9 < rows) pieces(8);
+      BT(3);
+      wait_vm0();  // this phase's DMA has landed
+    } else {
+      // output rows start at global row G-9: MID slot of the row above it,
+      // its image-local row and image ordinal
+      const int S_mid = pos_mod(G - 10, NR), rr0 = pos_mod(G - 9, LW), jm0 = (G - 9 - rr0) / LW;
+      struct Job2 {
+        unsigned ra[2][3];
+        int8_t* dst[2];
+        v4i rq[2];
+      };
+      // tap rows and output pointers of job j, and its residual (the block
+      // input, 16 channels of this lane) loaded one job ahead; conv2 waves
+      // issue no LDS-DMA, so these counted waits never wait for one
+      auto prep2 = [&](int j, Job2& q) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          int ro, col;
+          pix_of(j, t, ro, col);
+          const int R = G - 9 + ro;
+          const bool valid = R >= 0 && R < rows;
+          int r = rr0 + ro, jm = jm0;
+          if (r >= LW) {
+            r -= LW;
+            ++jm;
+          }
+          int s0 = S_mid + ro;
+          if (s0 >= NR) s0 -= NR;
+          row_addrs(OFF_MID, s0, r, col, valid, q.ra[t]);
+          const size_t pix = valid ? ((size_t)(b + jm * NG) * LW + r) * LW + col : 0;
+          if constexpr (BL1_TEST == 7)
+            q.rq[t] = v4i{0, 0, 0, 0};
+          else
+            q.rq[t] = gload16_untracked(a.x + pix * LC + h * 32 + lh * 16);
+          q.dst[t] = valid ? a.y + pix * LC + h * 32 + lh * 16 : g_trash_b + lane * 16;
+        }
+      };
+      auto live = [&](int j) {  // some pixel of job j exists (wave-uniform)
+        const int R0 = G - 9 + (j * 64) / LW, R1 = G - 9 + (j * 64 + 63) / LW;
+        return j < 7 && R1 >= 0 && R0 < rows && BL1_TEST != 1;
+      };
+      int j = j0;
+      while (j < 7 && !live(j)) j += 2;
+      Job2 cur, nxt;
+      if (j < 7) prep2(j, cur);
+      bool stored = false;  // stores of a previous job were issued after cur.rq
+      while (j < 7) {
+        v16i acc[2];
+        BT(0);
+        run_job(cur.ra[0], cur.ra[1], acc);
+        BT(1);
+        int jn = j + 2;
+        while (jn < 7 && !live(jn)) jn += 2;
+        if (jn < 7) prep2(jn, nxt);  // next job's residual loads
+        // VM ops younger than cur.rq: the previous job's 2 stores, nxt.rq
+        const int younger = (stored ? 2 : 0) + (jn < 7 ? 2 : 0);
+        if (younger == 4)
+          wait_vm_tie<4>(cur.rq[0], cur.rq[1]);
+        else if (younger == 2)
+          wait_vm_tie<2>(cur.rq[0], cur.rq[1]);
+        else
+          wait_vm_tie<0>(cur.rq[0], cur.rq[1]);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          int8_t* d = cur.dst[t];
+          if constexpr (BL1_TEST == 8) d = g_trash_b + lane * 16;
+          *(v4i*)d = epilogue(acc[t], true, cur.rq[t]);
+        }
+        stored = true;
+        BT(2);
+        if (jn < 7) cur = nxt;
+        j = jn;
+      }
+      BT(3);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): intermediate rows written (vmcnt untouched)
+    __builtin_amdgcn_s_barrier();
+    BT(4);
+  }
+  BT_STORE();
+  wait_vm0();
+}
+
+int num_cus_b() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+}  // namespace
+
+bool block_l1_shape(int C, int OC, int H, int W) { return C == LC && OC == LC && H == LW && W == LW; }
+
+hipError_t launch_block_l1(const int8_t* x, int N, const int8_t* w1, const float* a1, const float* b1,
+                           const int8_t* w2, const float* a2, const float* b2, float s_res, int8_t* y,
+                           hipStream_t s) {
+  if (N <= 0) return hipSuccess;
+  BlockArgs a{x, y, w1, w2, a1, b1, a2, b2, s_res, N};
+  int grid = num_cus_b();
+  if (const char* e = std::getenv("DLQ_L1_GRID")) {  // test knob: several images per workgroup
+    const int g = std::atoi(e);
+    if (g > 0 && g < grid) grid = g;
+  }
+  hipLaunchKernelGGL(block_l1_kernel, dim3(N < grid ? N : grid), dim3(512), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace dlq

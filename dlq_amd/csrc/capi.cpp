@@ -273,6 +273,17 @@ int dlq_conv2d_s2_ds_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d_s2_ds launch: ") + hipGetErrorString(e));
 }
 
+int dlq_block_l1_nhwc_s8(const int8_t* x, int N, const int8_t* w1, const float* alpha1, const float* beta1,
+                         const int8_t* w2, const float* alpha2, const float* beta2, float s_res, int8_t* y,
+                         void* stream) {
+  if (N < 0) return fail(DLQ_ERR_ARG, "block_l1: bad batch");
+  if (N == 0) return DLQ_OK;
+  if (!x || !w1 || !alpha1 || !beta1 || !w2 || !alpha2 || !beta2 || !y)
+    return fail(DLQ_ERR_ARG, "block_l1: null pointer");
+  hipError_t e = launch_block_l1(x, N, w1, alpha1, beta1, w2, alpha2, beta2, s_res, y, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("block_l1 launch: ") + hipGetErrorString(e));
+}
+
 size_t dlq_stem_packed_bytes(void) { return stem_packed_bytes(); }
 
 int dlq_pack_stem_weights_s8(const int8_t* q_oihw, const float* alpha, int8_t* packed, float* alpha_packed) {

@@ -52,6 +52,12 @@ size_t downsample_packed_bytes(int OC, int C);
 void downsample_pack(const int8_t* q_oc_ic, int OC, int IC, int C, int8_t* out);
 hipError_t launch_conv3x3s2(const ConvArgs& a, const int8_t* w_ds, const float* alpha_ds, const float* beta_ds,
                             int8_t* y_ds, hipStream_t s);
+// Fused layer1 basic block (block_l1.hip): C == OC == 64 at 56x56, identity
+// skip; generic packed weights of both convs.
+bool block_l1_shape(int C, int OC, int H, int W);
+hipError_t launch_block_l1(const int8_t* x, int N, const int8_t* w1, const float* a1, const float* b1,
+                           const int8_t* w2, const float* a2, const float* b2, float s_res, int8_t* y,
+                           hipStream_t s);
 // Fused stem (stem.hip): quantise + conv1 7x7/s2 + BN/ReLU/requant + maxpool.
 size_t stem_packed_bytes();
 void pack_stem_weights(const int8_t* q_oihw, const float* alpha, int8_t* out, float* alpha_abs);

@@ -229,6 +229,21 @@ int conv_family(const ConvLayer& c, int H) {
   return DLQ_FAM_OTHER;
 }
 
+// The layer1 block runs as one fused launch (DLQ_BLOCK_UNFUSED=1: two conv
+// launches, for A/B timing).
+bool fused_l1_block(const dlq_resnet18* m, const Block& b, int H, int W) {
+  static const bool off = [] {
+    const char* e = std::getenv("DLQ_BLOCK_UNFUSED");
+    return e && e[0] == '1';
+  }();
+  if (off || b.down) return false;
+  const ConvLayer& c1 = m->convs[b.c1];
+  const ConvLayer& c2 = m->convs[b.c2];
+  return c1.k == 3 && c1.s == 1 && c1.p == 1 && c2.k == 3 && c2.s == 1 && c2.p == 1 &&
+         block_l1_shape(c1.Cstore, c1.OC, H, W) && block_l1_shape(c2.Cstore, c2.OC, H, W) &&
+         !wide_layout(c1.Cstore, c1.OC, H, W, 3, 3, 1, 1, 1, 1);
+}
+
 // basic_block_forward (infer_e2e.cu:156-203): conv-bn-relu, conv-bn,
 // identity | 1x1 downsample-bn, add, relu -- three launches at most.
 int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N, int H,
@@ -239,6 +254,18 @@ int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N
   const int8_t* skip = in;
   float s_skip = m->scales.at(c1.in_site);
   int rc;
+  if (fused_l1_block(m, b, H, W)) {
+    // both convs, the identity add and the ReLUs in one launch; the
+    // intermediate never leaves the CU (block_l1.hip)
+    const ConvLayer& c2 = m->convs[b.c2];
+    if ((rc = mark(m, s, DLQ_FAM_L1))) return rc;
+    const float r_s = dlq::res_scale(s_skip, m->scales.at(c2.site));
+    hipError_t e = launch_block_l1(in, N, c1.w, c1.alpha, c1.beta, c2.w, c2.alpha, c2.beta, r_s, out, s);
+    if (e != hipSuccess) return hip_fail(e, "block_l1 launch");
+    *OH = H;
+    *OW = W;
+    return DLQ_OK;
+  }
   if (b.down && m->convs[b.ds].wf && conv3x3s2_shape(c1.Cstore, c1.OC, H, W, 3, 3, 2, 2, 1, 1) &&
       wide_layout(c1.Cstore, c1.OC, H, W, 3, 3, 2, 2, 1, 1)) {
     // conv1 (3x3/s2) and the 1x1/s2 downsample in one launch
@@ -594,6 +621,11 @@ int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes)
     const int H = c1.H, OH = c2.H;
     const double mac1 = (double)c1.OC * c1.IC * 9 * OH * OH, mac2 = (double)c2.OC * c2.IC * 9 * OH * OH;
     const double in1 = (double)H * H * c1.IC, out = (double)OH * OH * c2.OC;
+    if (fused_l1_block(m, b, H, H)) {  // one launch: block input + output bytes
+      macs[DLQ_FAM_L1] += mac1 + mac2;
+      bytes[DLQ_FAM_L1] += in1 + out;
+      continue;
+    }
     if (b.down) {
       const ConvLayer& ds = m->convs[b.ds];
       macs[DLQ_FAM_S2DS] += mac1 + (double)ds.OC * ds.IC * OH * OH;

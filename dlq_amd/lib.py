@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(_HERE, "libdlq.so")
 DLQ_OK = 0
 DLQ_OUT_S8, DLQ_OUT_F32, DLQ_OUT_S32 = 0, 1, 2
 # kernel families of dlq_resnet18_timing (include/dlq.h DLQ_FAM_*)
-FAMILIES = ["stem_fused_kernel", "conv3x3s1_kernel (layer1)", "conv3x3s2_kernel (+downsample)",
+FAMILIES = ["stem_fused_kernel", "block_l1_kernel (layer1 block)", "conv3x3s2_kernel (+downsample)",
             "conv3x3w_kernel (layer2-4 s1)", "gap16_kernel", "linear_kernel (fc)", "other"]
 
 
@@ -62,6 +62,7 @@ _SIGS = {
     "dlq_basic_block_s8": ([_vp, _i, _vp, _i, _vp, _vp], _i),
     "dlq_downsample_packed_bytes": ([_i, _i], _sz),
     "dlq_pack_downsample_weights_s8": ([_vp, _i, _i, _i, _vp], _i),
+    "dlq_block_l1_nhwc_s8": ([_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, C.c_float, _vp, _vp], _i),
     "dlq_conv2d_s2_ds_nhwc_s8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "dlq_stem_packed_bytes": ([], _sz),
     "dlq_pack_stem_weights_s8": ([_vp, _vp, _vp, _vp], _i),

@@ -181,6 +181,19 @@ def conv2d_s2_ds_nhwc_s8(x: torch.Tensor, w_packed: torch.Tensor, alpha: torch.T
     return y, y_ds
 
 
+def block_l1_s8(x: torch.Tensor, w1: torch.Tensor, alpha1: torch.Tensor, beta1: torch.Tensor,
+                w2: torch.Tensor, alpha2: torch.Tensor, beta2: torch.Tensor, res_scale: float) -> torch.Tensor:
+    """Fused layer1 basic block on NHWC int8 x[N,56,56,64] (see include/dlq.h
+    dlq_block_l1_nhwc_s8); w1/w2 from pack_conv_weights(q, 64, 56, 1, 1)."""
+    _dev(x, torch.int8)
+    if tuple(x.shape[1:]) != (56, 56, 64):
+        raise ValueError(f"block_l1_s8: needs [N,56,56,64], got {tuple(x.shape)}")
+    y = torch.empty_like(x)
+    check(lib.dlq_block_l1_nhwc_s8(ptr(x), x.shape[0], ptr(w1), ptr(alpha1), ptr(beta1), ptr(w2), ptr(alpha2),
+                                   ptr(beta2), float(res_scale), ptr(y), stream_handle()), "block_l1_s8")
+    return y
+
+
 def linear_s8(x: torch.Tensor, w_packed: torch.Tensor, OC: int, alpha=None, beta=None,
               relu: bool = False, out_kind: int = DLQ_OUT_F32):
     _dev(x, torch.int8)

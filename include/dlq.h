@@ -196,6 +196,19 @@ int dlq_conv2d_s2_ds_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8
                              const float* alpha, const float* beta, const int8_t* w_ds, const float* alpha_ds,
                              const float* beta_ds, int8_t* y, int8_t* y_ds, void* stream);
 
+/* Fused layer1 basic block: int8 NHWC x[N][56][56][64] -> y (same shape) =
+ * ReLU(requant(BN2(conv2(h)) + s_res * x)), h = ReLU(requant(BN1(conv1(x)))),
+ * both convs 3x3/s1/p1 64->64, in ONE launch (the intermediate h stays in
+ * LDS; x is read once and is also the residual).  w1, w2: images from
+ * dlq_pack_conv_weights_s8 for the descriptor {N, 56, 56, 64, 64, 3, 3, 1, 1,
+ * 1, 1}; alpha/beta[64] in output-grid units (dlq_fold_bn); s_res =
+ * dlq_res_scale(s_x, s_y2).  Bit-identical to dlq_conv2d_nhwc_s8(conv1,
+ * relu) followed by dlq_conv2d_nhwc_s8(conv2, residual x, relu).  Replaces
+ * basic_block_forward (RK/runtime/infer_e2e.cu:156-203) for layer1.0/1.1. */
+int dlq_block_l1_nhwc_s8(const int8_t* x, int N, const int8_t* w1, const float* alpha1, const float* beta1,
+                         const int8_t* w2, const float* alpha2, const float* beta2, float s_res, int8_t* y,
+                         void* stream);
+
 /* Fused stem: fp32 NCHW x[N][3][224][224] -> int8 NHWC y[N][56][56][64] =
  * maxpool3x3s2p1(requant(ReLU(BN(conv7x7s2p3(quant(x)))))).  One launch
  * replaces the input upload + conv1 + bn1 + relu + maxpool sequence of
@@ -287,7 +300,7 @@ int dlq_resnet18_stage(dlq_resnet18* m, const char* name, void* dst, size_t cap,
  * and forward, the basis of a roofline's "achieved". */
 enum {
   DLQ_FAM_STEM = 0,  /* stem_fused_kernel: quantise + conv1 + BN/ReLU + maxpool */
-  DLQ_FAM_L1 = 1,    /* conv3x3s1_kernel: layer1 3x3 convs                      */
+  DLQ_FAM_L1 = 1,    /* block_l1_kernel: fused layer1 basic blocks             */
   DLQ_FAM_S2DS = 2,  /* conv3x3s2_kernel: layerX.0 conv1 + fused downsample     */
   DLQ_FAM_WIDE = 3,  /* conv3x3w_kernel: layer2-4 stride-1 3x3 convs            */
   DLQ_FAM_GAP = 4,   /* gap16_kernel                                            */
