@@ -343,15 +343,18 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
       // output rows start at global row G-9: MID slot of the row above it,
       // its image-local row and image ordinal
       const int S_mid = pos_mod(G - 10, NR), rr0 = pos_mod(G - 9, LW), jm0 = (G - 9 - rr0) / LW;
-      struct Job2 {
+      // per job: tap rows, output pointers and the residual (the block
+      // input, 16 channels of this lane, loaded before the job's MFMAs and
+      // awaited after them; conv2 waves issue no LDS-DMA, so the wait covers
+      // only these loads and the previous job's stores).  The loads land in
+      // registers no other code touches before the tied wait: no copies of
+      // in-flight registers.
+      for (int j = j0; j < 7; j += 2) {
+        const int R0 = G - 9 + (j * 64) / LW, R1 = G - 9 + (j * 64 + 63) / LW;
+        if (R1 < 0 || R0 >= rows || BL1_TEST == 1) continue;  // no pixel of this job exists (wave-uniform)
         unsigned ra[2][3];
         int8_t* dst[2];
         v4i rq[2];
-      };
-      // tap rows and output pointers of job j, and its residual (the block
-      // input, 16 channels of this lane) loaded one job ahead; conv2 waves
-      // issue no LDS-DMA, so these counted waits never wait for one
-      auto prep2 = [&](int j, Job2& q) {
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           int ro, col;
@@ -365,50 +368,26 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
           }
           int s0 = S_mid + ro;
           if (s0 >= NR) s0 -= NR;
-          row_addrs(OFF_MID, s0, r, col, valid, q.ra[t]);
+          row_addrs(OFF_MID, s0, r, col, valid, ra[t]);
           const size_t pix = valid ? ((size_t)(b + jm * NG) * LW + r) * LW + col : 0;
           if constexpr (BL1_TEST == 7)
-            q.rq[t] = v4i{0, 0, 0, 0};
+            rq[t] = v4i{0, 0, 0, 0};
           else
-            q.rq[t] = gload16_untracked(a.x + pix * LC + h * 32 + lh * 16);
-          q.dst[t] = valid ? a.y + pix * LC + h * 32 + lh * 16 : g_trash_b + lane * 16;
+            rq[t] = gload16_untracked(a.x + pix * LC + h * 32 + lh * 16);
+          dst[t] = valid ? a.y + pix * LC + h * 32 + lh * 16 : g_trash_b + lane * 16;
         }
-      };
-      auto live = [&](int j) {  // some pixel of job j exists (wave-uniform)
-        const int R0 = G - 9 + (j * 64) / LW, R1 = G - 9 + (j * 64 + 63) / LW;
-        return j < 7 && R1 >= 0 && R0 < rows && BL1_TEST != 1;
-      };
-      int j = j0;
-      while (j < 7 && !live(j)) j += 2;
-      Job2 cur, nxt;
-      if (j < 7) prep2(j, cur);
-      bool stored = false;  // stores of a previous job were issued after cur.rq
-      while (j < 7) {
         v16i acc[2];
         BT(0);
-        run_job(cur.ra[0], cur.ra[1], acc);
+        run_job(ra[0], ra[1], acc);
         BT(1);
-        int jn = j + 2;
-        while (jn < 7 && !live(jn)) jn += 2;
-        if (jn < 7) prep2(jn, nxt);  // next job's residual loads
-        // VM ops younger than cur.rq: the previous job's 2 stores, nxt.rq
-        const int younger = (stored ? 2 : 0) + (jn < 7 ? 2 : 0);
-        if (younger == 4)
-          wait_vm_tie<4>(cur.rq[0], cur.rq[1]);
-        else if (younger == 2)
-          wait_vm_tie<2>(cur.rq[0], cur.rq[1]);
-        else
-          wait_vm_tie<0>(cur.rq[0], cur.rq[1]);
+        wait_vm_tie<0>(rq[0], rq[1]);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          int8_t* d = cur.dst[t];
+          int8_t* d = dst[t];
           if constexpr (BL1_TEST == 8) d = g_trash_b + lane * 16;
-          *(v4i*)d = epilogue(acc[t], true, cur.rq[t]);
+          *(v4i*)d = epilogue(acc[t], true, rq[t]);
         }
-        stored = true;
         BT(2);
-        if (jn < 7) cur = nxt;
-        j = jn;
       }
       BT(3);
     }

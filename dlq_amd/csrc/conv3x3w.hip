@@ -263,7 +263,8 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
     // 9 taps x one 32-deep k-step.  Fragments are read two taps ahead; stage
     // s+2's DMA pieces go out one per tap between the MFMAs.
     const int sbase = (s % WRING) * STAGE;
-    v4i fa[3][WFM], fb[3][WFN];
+    constexpr int PD = (XB & 64) ? 3 : 2;  // prefetch distance in taps
+    v4i fa[PD + 1][WFM], fb[PD + 1][WFN];
     auto load_tap = [&](int tap, int buf) {
 #pragma unroll
       for (int fm = 0; fm < WFM; ++fm) fa[buf][fm] = *(const v4i*)(lds + sbase + a_off[fm] + tap * 32);
@@ -273,17 +274,17 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
     // DMA pieces of stage s+2 per tap (loader waves): pieces [t*DPW/9, (t+1)*DPW/9)
     auto run_taps = [&](auto mfma_on, auto ld) {
       constexpr bool LD = decltype(ld)::value;
-      load_tap(0, 0);
-      load_tap(1, 1);
+#pragma unroll
+      for (int t = 0; t < PD; ++t) load_tap(t, t);
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int k0 = tap * DPW / 9, k1 = (tap + 1) * DPW / 9;
-        if (tap + 2 < 9) load_tap(tap + 2, (tap + 2) % 3);
+        if (tap + PD < 9) load_tap(tap + PD, (tap + PD) % (PD + 1));
         if constexpr (LD) {
 #pragma unroll
           for (int k = k0; k < k1; ++k) issue_piece(s + 2, k);
         }
-        const int bu = tap % 3;
+        const int bu = tap % (PD + 1);
         if constexpr (decltype(mfma_on)::value) {
           if constexpr ((XB & 32) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -301,7 +302,7 @@ __global__ __launch_bounds__(WNW * 64, 1) void conv3x3w_kernel(ConvArgs a) {
         // interleave: the next fragments' ds_reads and this tap's DMA pieces between the MFMAs
         const int nv = LD ? k1 - k0 : 0;
         constexpr int NR = WFM + WFN, NM = WFM * WFN;
-        if (tap + 2 < 9) {
+        if (tap + PD < 9) {
 #pragma unroll
           for (int i = 0; i < NM; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA

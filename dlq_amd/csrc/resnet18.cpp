@@ -85,6 +85,11 @@ struct dlq_resnet18 {
   std::vector<hipEvent_t> ev;
   std::vector<int> ev_tag;  // family of the launch that follows, -1 = end of forward
   size_t ev_used = 0;
+  // half-batch split: a second stream runs the second half of the batch in
+  // its own half of every workspace buffer, so the two halves' launches
+  // interleave and fill each other's tail waves
+  hipStream_t s2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
 };
 
 namespace {
@@ -335,6 +340,13 @@ int dlq_resnet18_create(dlq_resnet18** out) {
 }
 
 void dlq_resnet18_destroy(dlq_resnet18* m) {
+  if (m && m->s2) {
+    (void)hipStreamSynchronize(m->s2);
+    (void)hipStreamDestroy(m->s2);
+    (void)hipEventDestroy(m->fork);
+    (void)hipEventDestroy(m->join);
+    m->s2 = nullptr;
+  }
   if (!m) return;
   for (hipEvent_t e : m->ev) (void)hipEventDestroy(e);
   free_all(m);
@@ -508,18 +520,22 @@ int dlq_basic_block_s8(dlq_resnet18* m, int block, const int8_t* x, int N, int8_
   return basic_block_forward(m, b, x, N, H, H, m->buf[2], m->buf[3], y, (hipStream_t)stream, &OH, &OW);
 }
 
-int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, void* stream) {
-  if (!m) return fail(DLQ_ERR_ARG, "forward: null model");
-  if (!m->prepared) return fail(DLQ_ERR_STATE, "forward: call dlq_resnet18_prepare first");
-  if (B < 0 || B > m->max_batch) return fail(DLQ_ERR_ARG, "forward: batch exceeds prepared max_batch");
-  if (B == 0) return DLQ_OK;  // empty batch: nothing to read or write
-  if (!x || !logits) return fail(DLQ_ERR_ARG, "forward: null argument");
-  hipStream_t s = (hipStream_t)stream;
+namespace {
+
+// One forward pass over images [img0, img0 + B) of the workspace partition
+// starting at image img0 (every buffer is sized max_batch x the largest
+// per-image activation, so partitions of disjoint image ranges never overlap).
+int forward_pass(dlq_resnet18* m, const float* x, int B, float* logits, hipStream_t s, size_t img0,
+                 bool record) {
   const size_t nB = (size_t)B;
+  constexpr size_t kAct = 56 * 56 * 64;  // largest per-image activation (buffer stride per image)
+  void* stream = s;
   int rc;
-  m->stage.clear();
   int H = 56, W = 56;
-  int8_t* cur = m->buf[0];
+  int ci = 0;  // index of the buffer holding the current activation
+  auto bufp = [&](int i) { return m->buf[i] + img0 * kAct; };
+  int8_t* cur = bufp(ci);
+  int8_t* gq = m->gq + img0 * 512;
   const ConvLayer& st = m->convs[m->stem];
   if (!unfused_stem()) {
     // 0+1) fused stem: quantise + conv 7x7/s2 + BN + ReLU + maxpool 3x3/s2
@@ -532,45 +548,89 @@ int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, 
     if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
     rc = dlq_quantize_nchw_to_nhwc_s8(x, B, 3, 224, 224, kStemC, inv_scale(m->scales.at("input")), m->xq, stream);
     if (rc) return rc;
-    m->stage["input_q"] = {m->xq, nB * 224 * 224 * kStemC};
+    if (record) m->stage["input_q"] = {m->xq, nB * 224 * 224 * kStemC};
     int CH, CW;
     if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
     rc = conv2d_nhwc_s8(m, st, m->xq, B, 224, 224, nullptr, 0.f, true, m->c1, s, &CH, &CW);
     if (rc) return rc;
-    m->stage["conv1"] = {m->c1, nB * CH * CW * 64};
+    if (record) m->stage["conv1"] = {m->c1, nB * CH * CW * 64};
     if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
     rc = dlq_maxpool2d_3x3_s2p1_nhwc_s8(m->c1, B, 64, CH, CW, cur, stream);
     if (rc) return rc;
   }
-  if ((rc = record_stage(m, "stem_pool", cur, nB * H * W * 64, s))) return rc;
+  if (record && (rc = record_stage(m, "stem_pool", cur, nB * H * W * 64, s))) return rc;
   // 2-5) layer1..layer4 (:300-415)
   for (size_t bi = 0; bi < m->blocks.size(); ++bi) {
     const Block& b = m->blocks[bi];
-    int8_t* fr[3];
+    int fi[3];
     int k = 0;
-    for (auto* p : m->buf)
-      if (p != cur && k < 3) fr[k++] = p;
+    for (int i = 0; i < 4; ++i)
+      if (i != ci && k < 3) fi[k++] = i;
     int OH, OW;
-    rc = basic_block_forward(m, b, cur, B, H, W, fr[0], fr[1], fr[2], s, &OH, &OW);
+    rc = basic_block_forward(m, b, cur, B, H, W, bufp(fi[0]), bufp(fi[1]), bufp(fi[2]), s, &OH, &OW);
     if (rc) return rc;
-    cur = fr[2];
+    ci = fi[2];
+    cur = bufp(ci);
     H = OH;
     W = OW;
-    if (b.name.size() == 8 && b.name[7] == '1')
+    if (record && b.name.size() == 8 && b.name[7] == '1')
       if ((rc = record_stage(m, b.name.substr(0, 6).c_str(), cur, nB * H * W * b.oc, s))) return rc;
   }
   // 6) GAP + FC (:417-433)
   const std::string last = m->convs[m->blocks.back().c2].site;
   const float k = (m->scales.at(last) / (float)(H * W)) / m->scales.at("gap");
   if ((rc = mark(m, s, DLQ_FAM_GAP))) return rc;
-  rc = dlq_gap_nhwc_s8(cur, B, 512, H * W, k, m->gq, stream);
+  rc = dlq_gap_nhwc_s8(cur, B, 512, H * W, k, gq, stream);
   if (rc) return rc;
-  m->stage["gap"] = {m->gq, nB * 512};
+  if (record) m->stage["gap"] = {gq, nB * 512};
   if ((rc = mark(m, s, DLQ_FAM_FC))) return rc;
-  rc = dlq_linear_s8(m->gq, B, 512, m->fc_w, 1000, m->fc_alpha, m->fc_beta, 0, DLQ_OUT_F32,
-                     logits, stream);
+  rc = dlq_linear_s8(gq, B, 512, m->fc_w, 1000, m->fc_alpha, m->fc_beta, 0, DLQ_OUT_F32, logits, stream);
   if (rc) return rc;
-  if ((rc = mark(m, s, -1))) return rc;
+  return mark(m, s, -1);
+}
+
+// Split a batch into two halves on two streams (DLQ_SPLIT=1; measured within
+// 1% of the single stream at B=256, so off by default)?  Never while timing
+// launches (the per-launch events assume one stream) or keeping stage dumps,
+// and only for batches big enough that a half still fills the chip.
+bool use_split(const dlq_resnet18* m, int B) {
+  static const bool on = [] {
+    const char* e = std::getenv("DLQ_SPLIT");
+    return e && e[0] == '1';
+  }();
+  return on && !m->timing && !m->keep && B >= 64;
+}
+
+}  // namespace
+
+int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, void* stream) {
+  if (!m) return fail(DLQ_ERR_ARG, "forward: null model");
+  if (!m->prepared) return fail(DLQ_ERR_STATE, "forward: call dlq_resnet18_prepare first");
+  if (B < 0 || B > m->max_batch) return fail(DLQ_ERR_ARG, "forward: batch exceeds prepared max_batch");
+  if (B == 0) return DLQ_OK;  // empty batch: nothing to read or write
+  if (!x || !logits) return fail(DLQ_ERR_ARG, "forward: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  m->stage.clear();
+  int rc;
+  if (!use_split(m, B)) {
+    if ((rc = forward_pass(m, x, B, logits, s, 0, true))) return rc;
+  } else {
+    hipError_t e = hipSuccess;
+    if (!m->s2) {
+      if ((e = hipStreamCreateWithFlags(&m->s2, hipStreamNonBlocking)) != hipSuccess ||
+          (e = hipEventCreateWithFlags(&m->fork, hipEventDisableTiming)) != hipSuccess ||
+          (e = hipEventCreateWithFlags(&m->join, hipEventDisableTiming)) != hipSuccess)
+        return hip_fail(e, "split stream setup");
+    }
+    const int h1 = B / 2, h2 = B - h1;
+    if ((e = hipEventRecord(m->fork, s)) != hipSuccess || (e = hipStreamWaitEvent(m->s2, m->fork, 0)) != hipSuccess)
+      return hip_fail(e, "split fork");
+    if ((rc = forward_pass(m, x + (size_t)h1 * 3 * 224 * 224, h2, logits + (size_t)h1 * 1000, m->s2, h1, false)))
+      return rc;
+    if ((rc = forward_pass(m, x, h1, logits, s, 0, false))) return rc;
+    if ((e = hipEventRecord(m->join, m->s2)) != hipSuccess || (e = hipStreamWaitEvent(s, m->join, 0)) != hipSuccess)
+      return hip_fail(e, "split join");
+  }
   m->last_B = B;
   return DLQ_OK;
 }

@@ -270,6 +270,31 @@ def test_resnet18_batch_invariance_full_batch(gpu):
     assert np.array_equal(ref.view(np.int32), big[[0, 255]].view(np.int32))
 
 
+def test_resnet18_half_batch_split_matches_single_stream(gpu, monkeypatch):
+    """With DLQ_SPLIT=1, batches >= 64 run as two half-batches on two streams
+    (separate halves of every workspace buffer); an odd batch must give the
+    same logits as the single-stream pass (per-launch timing forces it).
+    The switch is read once per process: this runs in a child process."""
+    import subprocess
+    import sys
+    code = ("import numpy as np; from tests.test_gpu_parity import _split_case; _split_case()")
+    env = dict(__import__("os").environ, DLQ_SPLIT="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def _split_case():
+    from dlq_amd.models import ResNet18Int8, synthetic_images
+    sd, scales = model_and_scales()
+    x = synthetic_images(97, seed=7).cuda()
+    model = ResNet18Int8(sd, scales, max_batch=128)
+    split = model(x).cpu().numpy()
+    model.set_timing(True)
+    single = model(x).cpu().numpy()
+    model.set_timing(False)
+    assert np.array_equal(split.view(np.int32), single.view(np.int32))
+
+
 def test_resnet18_empty_and_oversize_batch(gpu):
     from dlq_amd.lib import DLQError
     from dlq_amd.models import ResNet18Int8

@@ -1,4 +1,4 @@
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp
-for a in "7 0" "7 17" "7 1" "7 16" "28 0" "28 17"; do
-timeout -k 10 60 tools/probe/conv3x3w_stamps $a || exit 1
-done
+for W in 7 14 28; do for xb in 0 64 96 0 64; do
+timeout -k 10 60 tools/probe/conv3x3w_nostamp $W $xb || exit 1
+done; done

@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
     else if (W == 14) hipLaunchKernelGGL((conv3x3w_kernel<14, 256, 0, true, v>), dim3(grid), dim3(WNW * 64), 0, 0, a); \
     else hipLaunchKernelGGL((conv3x3w_kernel<28, 128, 0, true, v>), dim3(grid), dim3(WNW * 64), 0, 0, a); \
     break;
-    switch (dbg) { XBCASE(0) XBCASE(1) XBCASE(2) XBCASE(3) XBCASE(4) XBCASE(5) XBCASE(6) XBCASE(7) XBCASE(16) XBCASE(17) XBCASE(32) XBCASE(48) }
+    switch (dbg) { XBCASE(0) XBCASE(1) XBCASE(2) XBCASE(3) XBCASE(4) XBCASE(5) XBCASE(6) XBCASE(7) XBCASE(16) XBCASE(17) XBCASE(32) XBCASE(48) XBCASE(64) XBCASE(96) }
   };
   for (int it = 0; it < 3; ++it) launch();
   hipEventRecord(e0, 0);
