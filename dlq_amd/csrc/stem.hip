@@ -46,6 +46,31 @@ constexpr int LDS_STEM = OFF_STAGE + SNW * 512;
 static_assert(LDS_STEM <= 160 * 1024, "LDS budget");
 constexpr int kIntMin = (int)0x80000000;
 
+#ifdef DLQ_STAMPS
+// timing-probe builds: per-wave cycle totals by section (no VM ops in the loop)
+__device__ unsigned long long g_sstamps[512 * 8 * 8];
+#define ST_DECL unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime()
+#define ST(k)                                                       \
+  do {                                                              \
+    const unsigned long long st_now = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += st_now - st_prev;                                  \
+    st_prev = st_now;                                               \
+  } while (0)
+#define ST_STORE()                                                                                       \
+  do {                                                                                                   \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 512)                                                     \
+      for (int q_ = 0; q_ < 6; ++q_) g_sstamps[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + q_] = st_acc[q_]; \
+  } while (0)
+#else
+#define ST_DECL
+#define ST(k) \
+  do {        \
+  } while (0)
+#define ST_STORE() \
+  do {             \
+  } while (0)
+#endif
+
 struct StemArgs {
   const float* x;      // [N][3][224][224]
   const int8_t* w;     // [64][16 super taps][16 B] (dlq_pack_stem_weights_s8)
@@ -84,6 +109,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
   const int a_unit = 28 * q + 1 + pi;  // super-col unit of tap kx = 0 (unit = super col + 4)
   int8_t* stg = lds + OFF_STAGE + wave * 512;
 
+  ST_DECL;
   for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
     const int n = item / a.nb, band = item - n * a.nb;
     const int py0 = band * a.R, py1 = min(56, py0 + a.R);
@@ -108,35 +134,31 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
         }
       }
     };
-    // Quantise raw pair k into two super rows of the patch ring: waves 0-1
-    // the first row, waves 2-3 the second; 128 units = super cols -4..123.
+    // Quantise raw pair k into two super rows of the patch ring, all 8 waves:
+    // thread = (pixel row dy, super row h, unit); 128 units = super cols
+    // -4..123; each thread writes the 8 bytes of its dy (dx = 0, 1).
     auto convert_pair = [&](int k) {
-      if (wave >= 4) return;
-      const int h = wave >> 1, unit = tid & 127, sc = unit - 4;
+      const int unit = tid & 127, h = (tid >> 7) & 1, dy = tid >> 8, sc = unit - 4;
       const int sr = sr0 + 2 * k + h;
-      v4i out = {0, 0, 0, 0};
+      int2 out = {0, 0};
       if ((unsigned)sr < 112u && (unsigned)sc < 112u) {
         const int8_t* raw = lds + OFF_RAW + (k % RAW_SLOTS) * RAW_SLOT_BYTES + h * 6 * 1024 + sc * 8;
-        unsigned u[3][2][2];  // [c][dy][dx]: clamp(x/s) + 1.5*2^23 -> rne'd int8 in the low byte
+        unsigned u[3][2];  // [c][dx]: clamp(x/s) + 1.5*2^23 -> rne'd int8 in the low byte
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
+        for (int c = 0; c < 3; ++c) {
+          const int2 f = *(const int2*)(raw + (c * 2 + dy) * 1024);  // dx = 0, 1 (read as ints)
+          u[c][0] = __float_as_uint(__builtin_amdgcn_fmed3f(__int_as_float(f.x) * a.inv_s, -127.f, 127.f) +
+                                    12582912.0f);
+          u[c][1] = __float_as_uint(__builtin_amdgcn_fmed3f(__int_as_float(f.y) * a.inv_s, -127.f, 127.f) +
+                                    12582912.0f);
+        }
 #pragma unroll
-          for (int dy = 0; dy < 2; ++dy) {
-            const int2 f = *(const int2*)(raw + (c * 2 + dy) * 1024);  // dx = 0, 1 (read as ints)
-            u[c][dy][0] = __float_as_uint(
-                __builtin_amdgcn_fmed3f(__int_as_float(f.x) * a.inv_s, -127.f, 127.f) + 12582912.0f);
-            u[c][dy][1] = __float_as_uint(
-                __builtin_amdgcn_fmed3f(__int_as_float(f.y) * a.inv_s, -127.f, 127.f) + 12582912.0f);
-          }
-#pragma unroll
-        for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-          for (int dx = 0; dx < 2; ++dx) {  // bytes (c0, c1, c2, 0)
-            const unsigned t = __builtin_amdgcn_perm(u[1][dy][dx], u[0][dy][dx], 0x0c0c0400u);
-            out[dy * 2 + dx] = (int)__builtin_amdgcn_perm(u[2][dy][dx], t, 0x0c040100u);
-          }
+        for (int dx = 0; dx < 2; ++dx) {  // bytes (c0, c1, c2, 0)
+          const unsigned t = __builtin_amdgcn_perm(u[1][dx], u[0][dx], 0x0c0c0400u);
+          (dx ? out.y : out.x) = (int)__builtin_amdgcn_perm(u[2][dx], t, 0x0c040100u);
+        }
       }
-      *(v4i*)(lds + OFF_PATCH + (sr & (PATCH_SLOTS - 1)) * PATCH_ROW + unit * 16) = out;
+      *(int2*)(lds + OFF_PATCH + (sr & (PATCH_SLOTS - 1)) * PATCH_ROW + unit * 16 + dy * 8) = out;
     };
     // One conv row (global row oy): the wave's 32 px x 32 oc tile, 8 k-steps.
     auto conv_row = [&](int oy) {
@@ -193,14 +215,19 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
       // Pair t+3 (super rows 2p+3, 2p+4) has landed once only the younger VM
       // ops remain: pairs t+4 .. t+2+SLA and the output stores of the last
       // min(t, SLA) steps.
+      ST(5);
       wait_vm((SLA - 1) * D + (t < SLA ? t : SLA));
       __builtin_amdgcn_s_barrier();
+      ST(0);
       convert_pair(t + 3);
+      ST(1);
       issue_pair(t + 3 + SLA);
+      ST(2);
 
       int He[8], Ho[8];
       hpool(conv_row(2 * p), He);
       hpool(conv_row(2 * p + 1), Ho);
+      ST(3);
       // vertical max, epilogue on the pooled values, bytes -> staging [16 px][32 oc]
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
@@ -214,10 +241,12 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
       const int pxl = lane >> 1, hf = lane & 1;
       const v4i o = *(const v4i*)(stg + pxl * 32 + hf * 16);
       if (lane < 28) *(v4i*)(a.y + (((size_t)n * 56 + p) * 56 + 14 * q + pxl) * 64 + ot * 32 + hf * 16) = o;
+      ST(4);
     }
     wait_vm0();
     __syncthreads();  // ring reuse by the next item
   }
+  ST_STORE();
 }
 
 int num_cus_stem() {
