@@ -191,6 +191,17 @@ int dlq_quantize_rows_s8(const float* x, int rows, int cols, int ldy, float inv_
 }
 
 namespace {
+// Stride-1 wide convs: the 392-px item kernel (conv3x3i.hip); DLQ_WIDE_256=1
+// selects the earlier 256-px item kernel (conv3x3w.hip, same weight image)
+// for A/B timing.
+hipError_t launch_wide_s1(const ConvArgs& a, hipStream_t s) {
+  static const bool v256 = [] {
+    const char* e = std::getenv("DLQ_WIDE_256");
+    return e && e[0] == '1';
+  }();
+  return v256 ? launch_conv3x3w(a, s) : launch_conv3x3i(a, s);
+}
+
 // Validation + ConvArgs of one conv launch (shared by the conv entry points).
 int conv_args(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
               const float* beta, const int8_t* residual, float res_scale, int relu, int out_kind, void* y,
@@ -242,7 +253,7 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
   if (a.P == 0) return DLQ_OK;
   hipError_t e = !wide ? launch_conv(a, (hipStream_t)stream)
                  : a.sH == 2 ? launch_conv3x3s2(a, nullptr, nullptr, nullptr, nullptr, (hipStream_t)stream)
-                             : launch_conv3x3w(a, (hipStream_t)stream);
+                             : launch_wide_s1(a, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d launch: ") + hipGetErrorString(e));
 }
 

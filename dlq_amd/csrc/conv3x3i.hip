@@ -1,0 +1,466 @@
+// conv3x3i.hip -- stride-1 3x3 int8 conv for the wide layers (C == OC in
+// {128, 256, 512} at 28x28 / 14x14 / 7x7: the nine layer2..layer4 launches
+// that keep the resolution), work items sized so that a B=256 launch is
+// exactly one or two items per CU.
+//
+// Replaces im2col_nchw + sgemm_tiled + bn/add/relu (RK/kernels/im2col.cu:5-58,
+// sgemm_tiled.cu:5-46; launched from RK/runtime/infer_e2e.cu:102-136,156-203)
+// for these shapes.  D[oc][px] = W[oc][(tap, c)] . X[px][(tap, c)], the
+// im2col formed in LDS from a once-loaded input patch per 32-channel slice.
+//
+// Work item = OT output channels x 392 consecutive output pixels (14 rows of
+// 28, one 14x14 image pair or eight 7x7 images: always whole output rows), so
+// P = 256 * H * W splits into 512 / 128 / 32 pixel ranges and, with OT = 128 /
+// 128 / 64, into 512 / 256 / 256 items: no tail round on 256 CUs.  392 px =
+// 13 MFMA pixel tiles (6 % padding, vs 23 % for 256-px items whose count does
+// not divide the CU count).
+//
+// LDS patch: per image chunk its rows plus a zero halo row above and below,
+// each row with a zero column on both sides, stored as two 16-channel planes
+// (plane = lane half of the MFMA operand).  Every tap of a pixel is then the
+// pixel's base unit + a compile-time offset (kh * (W + 2) + kw): ds_read_b128
+// with an immediate offset, no masks, no per-tap address arithmetic; the zero
+// halo comes from a zero source in global memory via the same LDS-DMA.
+//
+// Waves: the item's MT = OT/32 oc tiles x 13 px tiles are split so that the
+// two waves sharing a SIMD (w, w + 4) own 13 (MT = 4) or 7/6 (MT = 2) tiles
+// of one or two oc tiles: every SIMD does the same number of MFMAs per
+// k-step.  One A fragment + one B fragment per tile per tap.
+//
+// Stages (weight block [OT oc][9 taps x 32 B + 16 pad] + the patch of one
+// 32-channel slice) stream through a 2-slot LDS-DMA ring: stage s+1 is issued
+// right after the barrier that opens stage s, one piece per tap between the
+// MFMAs.  Epilogue as in conv3x3w.hip: MFMA-layout requantisation, two
+// v_permlane32_swap per tile, one 16-byte store per lane and tile.
+#include <type_traits>
+
+#include "device_common.h"
+
+namespace dlq {
+namespace {
+
+__device__ __attribute__((aligned(64))) int8_t g_trash_i[1024];  // sink for stores past the last pixel
+__device__ __attribute__((aligned(64))) int8_t g_zero_i[64];     // DMA source of the zero halo units
+
+// Cycle stamps for tools/probe/conv3x3i_stamps.hip (compiled out of the library).
+#ifdef DLQ_STAMPS
+__device__ unsigned long long g_stamps_i[256 * 8 * 64];
+#define ISTAMP(i)                                                                                  \
+  do {                                                                                             \
+    if ((threadIdx.x & 63) == 0 && (i) < 64)                                                       \
+      g_stamps_i[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define ISTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
+constexpr int IL = 392;        // output pixels per item
+constexpr int INT = 13;        // MFMA pixel tiles per item (416 >= 392)
+constexpr int ISC = 32;        // input channels per stage
+constexpr int IPITCH = 9 * ISC + 16;  // weight row pitch (304 B, odd multiple of 16: conflict-free)
+constexpr int INW = 8;         // waves per workgroup
+
+template <int W>
+struct IGeo {
+  static constexpr int H = W;
+  static constexpr int RPI = W < 14 ? W : 14;        // output rows per image chunk
+  static constexpr int IPI = IL / (RPI * W);          // image chunks per item (1, 2, 8)
+  static constexpr int OT = W == 7 ? 64 : 128;        // output channels per item
+  static constexpr int MT = OT / 32;                  // oc tiles per item
+  static constexpr int RW = W;                        // patch row pitch in units (compact rows)
+  static constexpr int UP = (IPI * (RPI + 2) * RW + 15) / 16 * 16;  // units per 16-channel plane
+  static constexpr int PP = (2 * UP + 63) / 64;       // patch DMA pieces (1 KiB)
+  static constexpr int ZU = 2 * W + 16;               // zero units read by the edge columns' side taps
+  static constexpr int WB = OT * IPITCH;              // weight bytes per stage
+  static constexpr int WP = WB / 1024;                // weight DMA pieces
+  static constexpr int NPIECE = WP + PP;
+  static constexpr int OFF_Z = WB + PP * 1024;        // zero region, inside each slot (slot-relative addresses)
+  static constexpr int SLOT = OFF_Z + (ZU * 16 + 255) / 256 * 256;
+  static constexpr int OFF_AB = 2 * SLOT;
+  static_assert(SLOT + 2 * W * 16 + 8 * 32 < 65536, "slot 1 + tap reached by a ds_read immediate offset");
+  static_assert(IPI * RPI * W == IL, "item = whole output rows");
+  static_assert(WB % 1024 == 0, "weight block = whole DMA pieces");
+};
+
+// Wave -> (oc tile, first px tile, px tile count).  MT = 4: SIMD pair (w, w+4)
+// = oc tile w&3, tiles [0,7) and [7,13).  MT = 2: oc tile w&1, tile groups
+// [0,4) [4,7) [7,10) [10,13) by w>>1, so the pair (w, w+4) owns 7 or 6.
+template <int MT>
+__device__ __forceinline__ void wave_tiles(int wave, int& mt, int& f0, int& nf) {
+  if constexpr (MT == 4) {
+    mt = wave & 3;
+    f0 = (wave >> 2) ? 7 : 0;
+    nf = (wave >> 2) ? 6 : 7;
+  } else {
+    mt = wave & 1;
+    const int g = wave >> 1;
+    f0 = g == 0 ? 0 : 1 + 3 * g;
+    nf = g == 0 ? 4 : 3;
+  }
+}
+
+// NLD loader waves issue the LDS-DMA (8: every wave; 4: only the waves of the
+// SIMD pairs with slack, see wave_tiles), lrank = this wave's rank among them.
+template <int W, int C, int OUT, bool RES, int NF, int NLD>
+__device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int mt, int f0, int lrank) {
+  using G = IGeo<W>;
+  constexpr int H = W, NS = C / ISC;
+  constexpr int OFF_AB = G::OFF_AB;
+  constexpr int DPW = (G::NPIECE + NLD - 1) / NLD;  // pieces per loader wave per stage
+  static_assert(DPW <= 18, "at most two DMA pieces per tap");
+  const bool loader = lrank >= 0;
+  constexpr int STORES = OUT == 0 ? NF : 4 * NF;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int n_ot = a.OCp / G::OT;
+  const int n_pi = (a.P + IL - 1) / IL;
+  const int NI = n_ot * n_pi;
+  const int Gd = gridDim.x, b = xcd_remap(blockIdx.x, Gd);
+  const int nst = ((NI - b + Gd - 1) / Gd) * NS;
+  const unsigned lds32 = lds_addr32(lds);
+
+  // item -> (oc tile, first pixel); pixel-range major so an XCD's items share input rows
+  auto item_of = [&](int li, int& ot, int& p0) {
+    const int it = b + li * Gd;
+    ot = it % n_ot;
+    p0 = (it / n_ot) * IL;
+  };
+
+  // ---- DMA issue side: pieces pc = wave + 8k; per lane the slice-0 source
+  // offset (weights: byte offset into a.w; patch: into a.x, -1 = zero unit).
+  int doff[DPW];
+  int iss_li = -1;
+  auto piece_of = [&](int k) {
+    const int pc = lrank + k * NLD;
+    return pc >= G::NPIECE ? pc - G::NPIECE : pc;  // past the end: re-issue an earlier piece
+  };
+  auto prep_issue = [&](int li) {
+    int ot, p0;
+    item_of(li, ot, p0);
+    const int R0 = p0 / W;  // first global output row of the item
+#pragma unroll
+    for (int k = 0; k < DPW; ++k) {
+      const int pc = piece_of(k);
+      if (pc < G::WP) {
+        // weight block [ot128][j][128][304]; a 64-oc item is half of one
+        const int o128 = (ot * G::OT) >> 7, ohalf = (ot * G::OT) & 127;
+        doff[k] = (o128 * NS * 128 + ohalf) * IPITCH + pc * 1024 + lane * 16;
+      } else {
+        const int u = (pc - G::WP) * 64 + lane;
+        const int plane = u >= G::UP ? 1 : 0, q = u - plane * G::UP;
+        const int c = q / ((G::RPI + 2) * G::RW), rem = q - c * ((G::RPI + 2) * G::RW);
+        const int r = rem / G::RW, iw = rem - r * G::RW;
+        const int gr = R0 + c * G::RPI;  // chunk's first global output row
+        const int n = gr / H, ih = gr - n * H + r - 1;
+        const bool ok = u < 2 * G::UP && n < a.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        doff[k] = ok ? ((n * H + ih) * W + iw) * C + plane * 16 : -1;
+      }
+    }
+  };
+  auto issue_piece = [&](int s, int k) {
+    const int sc = s < nst ? s : nst - 1;
+    const int j = sc % NS;
+    const int pc = piece_of(k);
+    const int8_t* src = pc < G::WP ? a.w + (size_t)(doff[k] + j * 128 * IPITCH)
+                                   : (doff[k] < 0 ? g_zero_i + (lane & 3) * 16 : a.x + (size_t)(doff[k] + j * ISC));
+    glds16_asm(src, lds32 + (s & 1) * G::SLOT + pc * 1024);
+  };
+  auto prep_for = [&](int s) {
+    const int sc = s < nst ? s : nst - 1;
+    const int li = sc / NS;
+    if (li != iss_li) {
+      prep_issue(li);
+      iss_li = li;
+    }
+  };
+
+  // ---- compute side
+  const int a_row = (mt * 32 + lr) * IPITCH + lh * 16;  // + slot + tap*32
+  // Per px tile the slot-0 byte offsets of its kw = 0 / 1 / 2 taps at kh = 0
+  // (kh rows and slot 1 are immediate offsets; item-invariant).  A pixel in
+  // the first / last column reads its kw = 0 / 2 taps from the slot's zero
+  // region instead, at the unit with the real address's bank.
+  int col_off[3][NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    int lp = (f0 + f) * 32 + lr;
+    lp = lp < IL ? lp : IL - 1;
+    const int c = lp / (G::RPI * W), rem = lp - c * (G::RPI * W);
+    const int r = rem / W, ow = rem - r * W;
+    const int bu = (c * (G::RPI + 2) + r) * G::RW + ow;  // tap (kh 0, kw 1): the pixel above
+    const int mid = G::WB + lh * G::UP * 16 + bu * 16;
+    col_off[1][f] = mid;
+    col_off[0][f] = ow == 0 ? G::OFF_Z + ((bu - 1) & 15) * 16 : mid - 16;
+    col_off[2][f] = ow == W - 1 ? G::OFF_Z + ((bu + 1) & 15) * 16 : mid + 16;
+  }
+  v16i acc[NF];
+  v4i rq[NF];
+  int cur_ot = 0, cur_p0 = 0;
+
+  ISTAMP(0);
+  if (loader) {
+    prep_for(0);
+#pragma unroll
+    for (int k = 0; k < DPW; ++k) issue_piece(0, k);
+  }
+
+  for (int s = 0; s < nst; ++s) {
+    const int li = s / NS, j = s - li * NS;
+    // Stage s has landed once every older VM op is done except the previous
+    // item's epilogue stores (issued after this stage's DMA).
+    if (j == 0 && s > 0)
+      wait_vm_const<STORES>();
+    else
+      wait_vm_const<0>();
+    __builtin_amdgcn_s_barrier();
+    ISTAMP(1 + 2 * s);
+    const bool more = s + 1 < nst;
+    if (more && loader) prep_for(s + 1);
+
+    if (j == 0) {
+      item_of(li, cur_ot, cur_p0);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) acc[f] = v16i{0};
+    }
+    const bool dma = more && loader && !(a.dbg & 2);
+    const int sb = (s & 1) * G::SLOT;
+    const int8_t* abase = lds + sb + a_row;
+    if (a.dbg & 4) {  // timing experiment: raise the non-loader waves' priority in the tap loop
+      if (!loader) __builtin_amdgcn_s_setprio(2);
+    }
+    // this stage's slot: move the tap base registers by one slot (each tap
+    // is then an immediate offset from them)
+    if (s > 0) {
+      const int d = (s & 1) ? G::SLOT : -G::SLOT;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        col_off[0][f] += d;
+        col_off[1][f] += d;
+        col_off[2][f] += d;
+      }
+    }
+    // A double-buffered per tap; each B fragment is re-loaded for the next
+    // tap right after the MFMA that consumed it (one register set per tile).
+    v4i fa[2], fb[NF];
+    auto ld_b = [&](int tap, int f) {
+      fb[f] = *(const v4i*)(lds + col_off[tap % 3][f] + (tap / 3) * G::RW * 16);
+    };
+    fa[0] = *(const v4i*)abase;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) ld_b(0, f);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int bu = tap & 1;
+      if (tap + 1 < 9) fa[bu ^ 1] = *(const v4i*)(abase + (tap + 1) * 32);
+      const int k0 = tap * DPW / 9, k1 = (tap + 1) * DPW / 9;
+      if (dma) {
+#pragma unroll
+        for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
+      }
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        acc[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu], fb[f], acc[f], 0, 0, 0);
+        if (tap + 1 < 9) ld_b(tap + 1, f);
+        if constexpr (OUT == 0 && RES) {
+          // the item's residual (store layout) into the registers this
+          // tile's last B fragment just freed; awaited in the epilogue
+          if (tap == 8 && j == NS - 1) {
+            const int p = cur_p0 + (f0 + f) * 32 + lr;
+            const bool keep = (f0 + f) * 32 + lr < IL && p < a.P;
+            const size_t off = keep ? (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16 : 0;
+            rq[f] = gload16_untracked(a.res + off);
+          }
+        }
+      }
+      if (tap + 1 < 9) {
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          if (i == 0)
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read (next tap's A + this tile's B)
+          else
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          if ((i == 1 && k1 > k0) || (i == 3 && k1 > k0 + 1))
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (LDS-DMA)
+        }
+      } else {
+        if (k1 > k0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        if (k1 > k0 + 1) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
+      }
+    }
+
+    if (a.dbg & 4) __builtin_amdgcn_s_setprio(0);
+    ISTAMP(2 + 2 * s);
+    if (j != NS - 1) continue;
+    // ---- fused epilogue of the item ----
+    if constexpr (OUT == 2) {
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int lp = (f0 + f) * 32 + lr, p = cur_p0 + lp;
+        const bool keep = lp < IL && p < a.P;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int oc = cur_ot * G::OT + mt * 32 + 8 * g + 4 * lh;
+          v4i* dst = keep ? (v4i*)((int*)a.y + (size_t)p * a.OC + oc) : (v4i*)(g_trash_i + lane * 16);
+          *dst = v4i{acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
+        }
+      }
+    } else {
+      const float lo = a.relu ? 0.f : -127.f;
+      float al[4][4], be[4][4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int oc = cur_ot * G::OT + mt * 32 + 8 * g + 4 * lh;
+        const v4i a4 = *(const v4i*)(lds + OFF_AB + oc * 4);
+        const v4i b4 = *(const v4i*)(lds + OFF_AB + (C + oc) * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          al[g][e] = __int_as_float(a4[e]);
+          be[g][e] = __int_as_float(b4[e]);
+        }
+      }
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        unsigned r[4] = {0, 0, 0, 0};
+        if constexpr (RES) {
+          // younger than rq[f]: rq[f+1..NF-1] and the stores of tiles 0..f-1
+          asm volatile("s_waitcnt vmcnt(%1)" : "+v"(rq[f]) : "n"(NF - 1) : "memory");
+          r[0] = (unsigned)rq[f][0];
+          r[1] = (unsigned)rq[f][1];
+          r[2] = (unsigned)rq[f][2];
+          r[3] = (unsigned)rq[f][3];
+          swap32(r[0], r[1]);
+          swap32(r[2], r[3]);
+        }
+        const unsigned rg[4] = {r[0], r[2], r[1], r[3]};
+        unsigned q[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = __builtin_fmaf((float)acc[f][4 * g + e], al[g][e], be[g][e]);
+            if constexpr (RES) v[e] = __builtin_fmaf((float)(int)(signed char)(rg[g] >> (8 * e)), a.s_res, v[e]);
+          }
+          q[g] = quant4(v[0], v[1], v[2], v[3], lo);
+        }
+        swap32(q[0], q[2]);
+        swap32(q[1], q[3]);
+        const int lp = (f0 + f) * 32 + lr, p = cur_p0 + lp;
+        const bool keep = lp < IL && p < a.P;
+        v4i* dst = keep ? (v4i*)((int8_t*)a.y + (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16)
+                        : (v4i*)(g_trash_i + lane * 16);
+        *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
+      }
+    }
+  }
+  ISTAMP(62);
+  wait_vm0();
+  ISTAMP(63);
+}
+
+template <int W, int C, int OUT, bool RES, int NLD>
+__global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
+  using G = IGeo<W>;
+  constexpr int OFF_AB = G::OFF_AB;
+  constexpr int LDS_TOTAL = OFF_AB + 2 * C * 4;
+  static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
+  const int tid = threadIdx.x;
+  if constexpr (OUT == 0) {
+    for (int i = tid; i < a.OCp; i += INW * 64) {
+      ((float*)(lds + OFF_AB))[i] = a.alpha[i];
+      ((float*)(lds + OFF_AB))[C + i] = a.beta[i];
+    }
+  }
+  for (int i = tid; i < G::ZU * 4; i += INW * 64) {
+    ((int*)(lds + G::OFF_Z))[i] = 0;
+    ((int*)(lds + G::SLOT + G::OFF_Z))[i] = 0;
+  }
+  __syncthreads();
+  int mt, f0, nf;
+  const int wave = tid >> 6;
+  wave_tiles<G::MT>(wave, mt, f0, nf);
+  // loader waves: all 8, or (NLD = 4) the SIMD pairs' less loaded side:
+  // MT = 4: waves 0-3 (7 tiles, which the SIMD's arbitration favours);
+  // MT = 2: waves 2, 3, 6, 7 (the two SIMDs with 6 tiles)
+  const int lrank4 = G::MT == 4 ? (wave < 4 ? wave : -1) : ((wave & 2) ? (wave & 1) + ((wave >> 2) << 1) : -1);
+  if constexpr (NLD == 8) {
+    if constexpr (G::MT == 4) {
+      if (nf == 7)
+        conv3x3i_body<W, C, OUT, RES, 7, 8>(a, lds, mt, f0, wave);
+      else
+        conv3x3i_body<W, C, OUT, RES, 6, 8>(a, lds, mt, f0, wave);
+    } else {
+      if (nf == 4)
+        conv3x3i_body<W, C, OUT, RES, 4, 8>(a, lds, mt, f0, wave);
+      else
+        conv3x3i_body<W, C, OUT, RES, 3, 8>(a, lds, mt, f0, wave);
+    }
+  } else {
+    if constexpr (G::MT == 4) {
+      if (nf == 7)
+        conv3x3i_body<W, C, OUT, RES, 7, 4>(a, lds, mt, f0, lrank4);
+      else
+        conv3x3i_body<W, C, OUT, RES, 6, 4>(a, lds, mt, f0, lrank4);
+    } else {
+      if (nf == 4)
+        conv3x3i_body<W, C, OUT, RES, 4, 4>(a, lds, mt, f0, lrank4);
+      else
+        conv3x3i_body<W, C, OUT, RES, 3, 4>(a, lds, mt, f0, lrank4);
+    }
+  }
+}
+
+int num_cus_i() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int W, int C>
+hipError_t launch_ci(const ConvArgs& a, hipStream_t s) {
+  using G = IGeo<W>;
+  const int NI = (a.OCp / G::OT) * ((a.P + IL - 1) / IL), ncu = num_cus_i();
+  const dim3 grid(NI < ncu ? NI : ncu), block(INW * 64);
+  if (a.dbg & 8) {  // timing experiment: 4 loader waves
+    if (a.out_kind == 2)
+      hipLaunchKernelGGL((conv3x3i_kernel<W, C, 2, false, 4>), grid, block, 0, s, a);
+    else if (a.res)
+      hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, true, 4>), grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, false, 4>), grid, block, 0, s, a);
+    return hipGetLastError();
+  }
+  if (a.out_kind == 2)
+    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 2, false, 8>), grid, block, 0, s, a);
+  else if (a.res)
+    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, true, 8>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, false, 8>), grid, block, 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// Same shapes and the same packed weight image as conv3x3w (conv3x3w_pack).
+hipError_t launch_conv3x3i(const ConvArgs& a, hipStream_t s) {
+  if (a.OCp != a.OC || a.C != a.OC || a.H != a.W) return hipErrorInvalidValue;
+  switch (a.W) {
+    case 28: return a.C == 128 ? launch_ci<28, 128>(a, s) : hipErrorInvalidValue;
+    case 14: return a.C == 256 ? launch_ci<14, 256>(a, s) : hipErrorInvalidValue;
+    case 7: return a.C == 512 ? launch_ci<7, 512>(a, s) : hipErrorInvalidValue;
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace dlq

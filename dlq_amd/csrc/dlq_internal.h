@@ -45,6 +45,8 @@ bool conv3x3w_shape(int C, int OC, int H, int W, int kH, int kW, int sH, int sW,
 size_t conv3x3w_packed_bytes(int OC, int C);
 void conv3x3w_pack(const int8_t* q_oihw, int OC, int IC, int C, int8_t* out);
 hipError_t launch_conv3x3w(const ConvArgs& a, hipStream_t s);
+// Same shapes and weight image, 392-px items (conv3x3i.hip).
+hipError_t launch_conv3x3i(const ConvArgs& a, hipStream_t s);
 // Stride-2 3x3 convs (conv3x3s2.hip), wide weight layout, optional fused 1x1/s2
 // downsample (w_ds == nullptr: conv only).
 bool conv3x3s2_shape(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW);
