@@ -101,8 +101,8 @@ __device__ __forceinline__ void wave_tiles(int wave, int& mt, int& f0, int& nf) 
   }
 }
 
-// NLD loader waves issue the LDS-DMA (8: every wave; 4: only the waves of the
-// SIMD pairs with slack, see wave_tiles), lrank = this wave's rank among them.
+// NLD loader waves issue the LDS-DMA, lrank = this wave's rank among them
+// (every wave: handing the DMA to the pairs' less loaded waves measured slower).
 template <int W, int C, int OUT, bool RES, int NF, int NLD>
 __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int mt, int f0, int lrank) {
   using G = IGeo<W>;
@@ -228,9 +228,6 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     const bool dma = more && loader && !(a.dbg & 2);
     const int sb = (s & 1) * G::SLOT;
     const int8_t* abase = lds + sb + a_row;
-    if (a.dbg & 4) {  // timing experiment: raise the non-loader waves' priority in the tap loop
-      if (!loader) __builtin_amdgcn_s_setprio(2);
-    }
     // this stage's slot: move the tap base registers by one slot (each tap
     // is then an immediate offset from them)
     if (s > 0) {
@@ -293,7 +290,6 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       }
     }
 
-    if (a.dbg & 4) __builtin_amdgcn_s_setprio(0);
     ISTAMP(2 + 2 * s);
     if (j != NS - 1) continue;
     // ---- fused epilogue of the item ----
@@ -363,7 +359,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   ISTAMP(63);
 }
 
-template <int W, int C, int OUT, bool RES, int NLD>
+template <int W, int C, int OUT, bool RES>
 __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   using G = IGeo<W>;
   constexpr int OFF_AB = G::OFF_AB;
@@ -385,34 +381,16 @@ __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   int mt, f0, nf;
   const int wave = tid >> 6;
   wave_tiles<G::MT>(wave, mt, f0, nf);
-  // loader waves: all 8, or (NLD = 4) the SIMD pairs' less loaded side:
-  // MT = 4: waves 0-3 (7 tiles, which the SIMD's arbitration favours);
-  // MT = 2: waves 2, 3, 6, 7 (the two SIMDs with 6 tiles)
-  const int lrank4 = G::MT == 4 ? (wave < 4 ? wave : -1) : ((wave & 2) ? (wave & 1) + ((wave >> 2) << 1) : -1);
-  if constexpr (NLD == 8) {
-    if constexpr (G::MT == 4) {
-      if (nf == 7)
-        conv3x3i_body<W, C, OUT, RES, 7, 8>(a, lds, mt, f0, wave);
-      else
-        conv3x3i_body<W, C, OUT, RES, 6, 8>(a, lds, mt, f0, wave);
-    } else {
-      if (nf == 4)
-        conv3x3i_body<W, C, OUT, RES, 4, 8>(a, lds, mt, f0, wave);
-      else
-        conv3x3i_body<W, C, OUT, RES, 3, 8>(a, lds, mt, f0, wave);
-    }
+  if constexpr (G::MT == 4) {
+    if (nf == 7)
+      conv3x3i_body<W, C, OUT, RES, 7, 8>(a, lds, mt, f0, wave);
+    else
+      conv3x3i_body<W, C, OUT, RES, 6, 8>(a, lds, mt, f0, wave);
   } else {
-    if constexpr (G::MT == 4) {
-      if (nf == 7)
-        conv3x3i_body<W, C, OUT, RES, 7, 4>(a, lds, mt, f0, lrank4);
-      else
-        conv3x3i_body<W, C, OUT, RES, 6, 4>(a, lds, mt, f0, lrank4);
-    } else {
-      if (nf == 4)
-        conv3x3i_body<W, C, OUT, RES, 4, 4>(a, lds, mt, f0, lrank4);
-      else
-        conv3x3i_body<W, C, OUT, RES, 3, 4>(a, lds, mt, f0, lrank4);
-    }
+    if (nf == 4)
+      conv3x3i_body<W, C, OUT, RES, 4, 8>(a, lds, mt, f0, wave);
+    else
+      conv3x3i_body<W, C, OUT, RES, 3, 8>(a, lds, mt, f0, wave);
   }
 }
 
@@ -432,21 +410,12 @@ hipError_t launch_ci(const ConvArgs& a, hipStream_t s) {
   using G = IGeo<W>;
   const int NI = (a.OCp / G::OT) * ((a.P + IL - 1) / IL), ncu = num_cus_i();
   const dim3 grid(NI < ncu ? NI : ncu), block(INW * 64);
-  if (a.dbg & 8) {  // timing experiment: 4 loader waves
-    if (a.out_kind == 2)
-      hipLaunchKernelGGL((conv3x3i_kernel<W, C, 2, false, 4>), grid, block, 0, s, a);
-    else if (a.res)
-      hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, true, 4>), grid, block, 0, s, a);
-    else
-      hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, false, 4>), grid, block, 0, s, a);
-    return hipGetLastError();
-  }
   if (a.out_kind == 2)
-    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 2, false, 8>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 2, false>), grid, block, 0, s, a);
   else if (a.res)
-    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, true, 8>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, true>), grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, false, 8>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, false>), grid, block, 0, s, a);
   return hipGetLastError();
 }
 

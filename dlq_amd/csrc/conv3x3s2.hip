@@ -19,6 +19,8 @@
 // bit 3 of the position, as in conv3x3w.hip).  Two-slot LDS-DMA ring (the
 // stride-2 patch is twice the stride-1 one), exact vmcnt counts, epilogue
 // through v_permlane32_swap into 16-byte stores.
+#include <cstdlib>
+
 #include "device_common.h"
 
 namespace dlq {
@@ -354,8 +356,15 @@ void downsample_pack(const int8_t* q, int OC, int IC, int C, int8_t* out) {
     }
 }
 
+// The 196-px item kernel (conv3x3s2i.hip) by default; DLQ_S2_128=1 keeps
+// this file's 128-px item kernel (same weight images) for A/B timing.
 hipError_t launch_conv3x3s2(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, const float* be_ds,
                             int8_t* y_ds, hipStream_t s) {
+  static const bool v128 = [] {
+    const char* e = std::getenv("DLQ_S2_128");
+    return e && e[0] == '1';
+  }();
+  if (!v128) return launch_conv3x3s2i(a, w_ds, al_ds, be_ds, y_ds, s);
   const int ncu = num_cus_s2();
   switch (a.W) {
     case 56: return launch_s2<28, 64>(a, w_ds, al_ds, be_ds, y_ds, s, ncu);

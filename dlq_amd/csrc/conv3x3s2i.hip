@@ -1,0 +1,375 @@
+// conv3x3s2i.hip -- stride-2 3x3 int8 conv (layer2.0 / layer3.0 / layer4.0
+// conv1: C -> 2C channels, resolution halved) with the block's 1x1/s2
+// downsample fused in, work items sized so that a B=256 launch is exactly
+// four, two or one items per CU.
+//
+// Replaces, per downsampling BasicBlock (RK = CUDA/resnet18-kernel-lab/cpp/fp32):
+// conv2d_nchw_im2col_gemm for conv1 + bn_launch + relu_forward
+// (RK/runtime/infer_e2e.cu:161-176) AND the downsample branch's conv2d + bn
+// (:187-196).  The 1x1/s2 downsample reads exactly conv1's centre tap
+// (kh = kw = 1), so its MFMA takes the B fragment conv1's tap 4 already holds.
+//
+// Work item = 128 output channels x 196 output pixels (7 output rows of 28,
+// one 14x14 image, or four 7x7 images: whole rows) -> 1024 / 512 / 256 items
+// at B = 256 (no tail round on 256 CUs), 7 MFMA pixel tiles (224 >= 196).
+// Waves: oc tile w & 3, pixel tiles [0,4) / [4,7) by w >> 2 (the SIMD pair
+// (w, w+4) owns all 7 of one oc tile); per tile a conv and a downsample
+// accumulator.
+//
+// LDS patch per 32-channel slice: each chunk's input rows 2*r0-1 .. 2*r1+1,
+// every row stored de-interleaved (even columns, then odd: kw = 1 reads
+// E[ow], kw = 2 O[ow], kw = 0 O[ow-1]) as two 16-channel planes, so all taps
+// of a pixel are one base register + immediate offsets and consecutive pixels
+// read consecutive 16-byte units; ow = 0's kw = 0 taps read a zero region on
+// the same banks.  Stage = conv1 weights [128][9 x 32 + 16] + downsample
+// weights [128][32 + 16] + patch; 2-slot LDS-DMA ring, the next stage issued
+// between the MFMAs right after the barrier that opens a stage.  Epilogues as
+// in conv3x3w.hip (permlane32 swaps into 16-byte stores).
+#include "device_common.h"
+
+namespace dlq {
+namespace {
+
+__device__ __attribute__((aligned(64))) int8_t g_trash_s2i[1024];
+__device__ __attribute__((aligned(64))) int8_t g_zero_s2i[64];
+
+constexpr int JL = 196;               // output pixels per item
+constexpr int JSC = 32;               // input channels per stage
+constexpr int JWP = 9 * JSC + 16;     // conv1 weight row pitch (304 B)
+constexpr int JDP = JSC + 16;         // downsample weight row pitch (48 B)
+constexpr int JNW = 8;                // waves
+constexpr int JOT = 128;              // output channels per item
+
+template <int OW, bool DS>
+struct JGeo {
+  static constexpr int OH = OW, WI = 2 * OW, HI = 2 * OH;  // output / input geometry
+  static constexpr int RPI = OW < 14 ? OW : (OW == 14 ? 14 : 7);  // output rows per chunk
+  static constexpr int IPI = JL / (RPI * OW);                 // chunks (images) per item
+  static constexpr int IRC = 2 * RPI + 1;                     // input rows per chunk
+  static constexpr int UP = (IPI * IRC * WI + 15) / 16 * 16;  // units per 16-channel plane
+  static constexpr int PP = (2 * UP + 63) / 64;               // patch DMA pieces
+  static constexpr int WB = JOT * JWP;                        // 38,912 = 38 pieces
+  static constexpr int DB = JOT * JDP;                        // 6,144 = 6 pieces
+  static constexpr int WP = (WB + (DS ? DB : 0)) / 1024;   // weight pieces (no downsample block without DS)
+  static constexpr int NPIECE = WP + PP;
+  static constexpr int OFF_P = WB + DB;                       // patch within a slot
+  static constexpr int ZU = 2 * WI + 16;                      // zero units (kh rows x bank spread)
+  static constexpr int OFF_Z = OFF_P + PP * 1024;
+  static constexpr int SLOT = OFF_Z + (ZU * 16 + 255) / 256 * 256;
+  static constexpr int OFF_AB = 2 * SLOT;                     // conv alpha/beta, then ds alpha/beta
+  static_assert(IPI * RPI * OW == JL, "item = whole output rows");
+  static_assert((WB + DB) % 1024 == 0, "weight blocks = whole DMA pieces");
+  static_assert((2 * WI + OW) * 16 < 65536, "tap offsets fit the ds_read immediate");
+};
+
+template <int OW, int C, int OUT, bool DS, int NF>
+__device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, int8_t* y_ds, int8_t* lds,
+                                         int mt, int f0) {
+  using G = JGeo<OW, DS>;
+  constexpr int NS = C / JSC, OC = 2 * C;
+  constexpr int DPW = (G::NPIECE + JNW - 1) / JNW;
+  static_assert(DPW <= 18, "at most two DMA pieces per tap");
+  constexpr int STORES = OUT == 0 ? (DS ? 2 * NF : NF) : 4 * NF;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int n_ot = a.OCp / JOT;
+  const int NI = n_ot * ((a.P + JL - 1) / JL);
+  const int Gd = gridDim.x, b = xcd_remap(blockIdx.x, Gd);
+  const int nst = ((NI - b + Gd - 1) / Gd) * NS;
+  const unsigned lds32 = lds_addr32(lds);
+
+  auto item_of = [&](int li, int& ot, int& p0) {
+    const int it = b + li * Gd;
+    ot = it % n_ot;
+    p0 = (it / n_ot) * JL;
+  };
+
+  // ---- DMA issue side (pieces pc = wave + 8k): conv weights, ds weights, patch
+  int doff[DPW];
+  int iss_li = -1;
+  auto piece_of = [&](int k) {
+    const int pc = wave + k * JNW;
+    return pc >= G::NPIECE ? pc - G::NPIECE : pc;
+  };
+  auto prep_issue = [&](int li) {
+    int ot, p0;
+    item_of(li, ot, p0);
+    const int R0 = p0 / OW;  // first global output row
+#pragma unroll
+    for (int k = 0; k < DPW; ++k) {
+      const int pc = piece_of(k);
+      if (pc < G::WB / 1024) {
+        doff[k] = ot * NS * G::WB + pc * 1024 + lane * 16;
+      } else if (pc < G::WP) {
+        doff[k] = ot * NS * G::DB + (pc - G::WB / 1024) * 1024 + lane * 16;
+      } else {
+        const int u = (pc - G::WP) * 64 + lane;
+        const int plane = u >= G::UP ? 1 : 0, q = u - plane * G::UP;
+        const int c = q / (G::IRC * G::WI), rem = q - c * (G::IRC * G::WI);
+        const int r = rem / G::WI, pos = rem - r * G::WI;
+        const int iw = pos < OW ? 2 * pos : 2 * (pos - OW) + 1;  // de-interleaved: even cols, then odd
+        const int gr = R0 + c * G::RPI;  // chunk's first global output row
+        const int n = gr / G::OH, ih = 2 * (gr - n * G::OH) - 1 + r;
+        const bool ok = u < 2 * G::UP && n < a.N && (unsigned)ih < (unsigned)G::HI;
+        doff[k] = ok ? ((n * G::HI + ih) * G::WI + iw) * C + plane * 16 : -1;
+      }
+    }
+  };
+  auto issue_piece = [&](int s, int k) {
+    const int sc = s < nst ? s : nst - 1;
+    const int j = sc % NS;
+    const int pc = piece_of(k);
+    const int8_t* src;
+    if (pc < G::WB / 1024)
+      src = a.w + (size_t)(doff[k] + j * G::WB);
+    else if (pc < G::WP)
+      src = w_ds + (size_t)(doff[k] + j * G::DB);
+    else
+      src = doff[k] < 0 ? g_zero_s2i + (lane & 3) * 16 : a.x + (size_t)(doff[k] + j * JSC);
+    const int dst = pc < G::WP ? pc * 1024 : G::OFF_P + (pc - G::WP) * 1024;
+    glds16_asm(src, lds32 + (s & 1) * G::SLOT + dst);
+  };
+  auto prep_for = [&](int s) {
+    const int sc = s < nst ? s : nst - 1;
+    const int li = sc / NS;
+    if (li != iss_li) {
+      prep_issue(li);
+      iss_li = li;
+    }
+  };
+
+  // ---- compute side: per px tile the slot-0 offsets of its kw = 1 (E[ow])
+  // and kw = 0 (O[ow-1] or the zero region) taps at kh = 0; kw = 2 (O[ow]) is
+  // kw = 1 + OW units, kh adds kh rows: immediate offsets.
+  const int a_row = (mt * 32 + lr) * JWP + lh * 16;
+  const int d_row = G::WB + (mt * 32 + lr) * JDP + lh * 16;
+  int mid_off[NF], left_off[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    int lp = (f0 + f) * 32 + lr;
+    lp = lp < JL ? lp : JL - 1;
+    const int c = lp / (G::RPI * OW), rem = lp - c * (G::RPI * OW);
+    const int r = rem / OW, ow = rem - r * OW;
+    const int bu = (c * G::IRC + 2 * r) * G::WI + ow;  // E[ow] of input row 2r-1
+    mid_off[f] = G::OFF_P + lh * G::UP * 16 + bu * 16;
+    left_off[f] = ow == 0 ? G::OFF_Z + ((bu + OW - 1) & 15) * 16 : mid_off[f] + (OW - 1) * 16;
+  }
+  v16i acc[NF], accd[DS ? NF : 1];
+  int cur_ot = 0, cur_p0 = 0;
+
+  prep_for(0);
+#pragma unroll
+  for (int k = 0; k < DPW; ++k) issue_piece(0, k);
+
+  for (int s = 0; s < nst; ++s) {
+    const int li = s / NS, j = s - li * NS;
+    if (j == 0 && s > 0)
+      wait_vm_const<STORES>();
+    else
+      wait_vm_const<0>();
+    __builtin_amdgcn_s_barrier();
+    const bool more = s + 1 < nst;
+    if (more) prep_for(s + 1);
+    if (j == 0) {
+      item_of(li, cur_ot, cur_p0);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        acc[f] = v16i{0};
+        if constexpr (DS) accd[f] = v16i{0};
+      }
+    }
+    const int sb = (s & 1) * G::SLOT;
+    if (s > 0) {
+      const int d = (s & 1) ? G::SLOT : -G::SLOT;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        mid_off[f] += d;
+        left_off[f] += d;
+      }
+    }
+    const int8_t* abase = lds + sb + a_row;
+    v4i fa[2], fb[NF], fd;
+    auto ld_b = [&](int tap, int f) {
+      const int kh = tap / 3, kw = tap % 3;
+      const int base = kw == 0 ? left_off[f] : mid_off[f];
+      fb[f] = *(const v4i*)(lds + base + (kh * G::WI + (kw == 2 ? OW : 0)) * 16);
+    };
+    fa[0] = *(const v4i*)abase;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) ld_b(0, f);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int bu = tap & 1;
+      if (tap + 1 < 9) fa[bu ^ 1] = *(const v4i*)(abase + (tap + 1) * 32);
+      if constexpr (DS) {
+        if (tap == 3) fd = *(const v4i*)(lds + sb + d_row);  // the downsample's A fragment, used at tap 4
+      }
+      const int k0 = tap * DPW / 9, k1 = (tap + 1) * DPW / 9;
+      if (more) {
+#pragma unroll
+        for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
+      }
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        acc[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu], fb[f], acc[f], 0, 0, 0);
+        if constexpr (DS) {
+          if (tap == 4) accd[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fd, fb[f], accd[f], 0, 0, 0);
+        }
+        if (tap + 1 < 9) ld_b(tap + 1, f);
+      }
+      if (tap + 1 < 9) {
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+          if (DS && tap == 4)
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA (conv + downsample)
+          else
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          if (i == 0 && DS && tap == 3)
+            __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // DS read: next A, ds A, B
+          else if (i == 0)
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read: next A, B
+          else
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          if ((i == 1 && k1 > k0) || (i == 2 && k1 > k0 + 1))
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (LDS-DMA)
+        }
+      } else {
+        if (k1 > k0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        if (k1 > k0 + 1) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
+      }
+    }
+
+    if (j != NS - 1) continue;
+    // ---- fused epilogues of the item ----
+    if constexpr (OUT == 2) {
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int lp = (f0 + f) * 32 + lr, p = cur_p0 + lp;
+        const bool keep = lp < JL && p < a.P;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int oc = cur_ot * JOT + mt * 32 + 8 * g + 4 * lh;
+          v4i* dst = keep ? (v4i*)((int*)a.y + (size_t)p * a.OC + oc) : (v4i*)(g_trash_s2i + lane * 16);
+          *dst = v4i{acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
+        }
+      }
+    } else {
+      auto epi = [&](const v16i* ac, int ab_off, float lo, int8_t* out) {
+        float al[4][4], be[4][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int oc = cur_ot * JOT + mt * 32 + 8 * g + 4 * lh;
+          const v4i a4 = *(const v4i*)(lds + G::OFF_AB + ab_off + oc * 4);
+          const v4i b4 = *(const v4i*)(lds + G::OFF_AB + ab_off + (OC + oc) * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            al[g][e] = __int_as_float(a4[e]);
+            be[g][e] = __int_as_float(b4[e]);
+          }
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          unsigned q[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf((float)ac[f][4 * g + e], al[g][e], be[g][e]);
+            q[g] = quant4(v[0], v[1], v[2], v[3], lo);
+          }
+          swap32(q[0], q[2]);
+          swap32(q[1], q[3]);
+          const int lp = (f0 + f) * 32 + lr, p = cur_p0 + lp;
+          const bool keep = lp < JL && p < a.P;
+          v4i* dst = keep ? (v4i*)(out + (size_t)p * a.OC + cur_ot * JOT + mt * 32 + lh * 16)
+                          : (v4i*)(g_trash_s2i + lane * 16);
+          *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
+        }
+      };
+      epi(acc, 0, a.relu ? 0.f : -127.f, (int8_t*)a.y);
+      if constexpr (DS) epi(accd, 2 * OC * 4, -127.f, y_ds);
+    }
+  }
+  wait_vm0();
+}
+
+// OUT: 0 = int8 (fused epilogues), 2 = int32 conv1 accumulators (DS = false).
+template <int OW, int C, int OUT, bool DS>
+__global__ __launch_bounds__(JNW * 64, 1) void conv3x3s2i_kernel(ConvArgs a, const int8_t* w_ds, const float* al_ds,
+                                                                 const float* be_ds, int8_t* y_ds) {
+  using G = JGeo<OW, DS>;
+  constexpr int OC = 2 * C;
+  constexpr int LDS_TOTAL = G::OFF_AB + (DS ? 4 : 2) * OC * 4;
+  static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
+  const int tid = threadIdx.x;
+  if constexpr (OUT == 0) {
+    float* ab = (float*)(lds + G::OFF_AB);
+    for (int i = tid; i < a.OCp; i += JNW * 64) {
+      ab[i] = a.alpha[i];
+      ab[OC + i] = a.beta[i];
+      if constexpr (DS) {
+        ab[2 * OC + i] = al_ds[i];
+        ab[3 * OC + i] = be_ds[i];
+      }
+    }
+  }
+  for (int i = tid; i < G::ZU * 4; i += JNW * 64) {
+    ((int*)(lds + G::OFF_Z))[i] = 0;
+    ((int*)(lds + G::SLOT + G::OFF_Z))[i] = 0;
+  }
+  __syncthreads();
+  const int wave = tid >> 6;
+  if (wave < 4)
+    s2i_body<OW, C, OUT, DS, 4>(a, w_ds, y_ds, lds, wave & 3, 0);
+  else
+    s2i_body<OW, C, OUT, DS, 3>(a, w_ds, y_ds, lds, wave & 3, 4);
+}
+
+int num_cus_s2i() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int OW, int C>
+hipError_t launch_j(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, const float* be_ds,
+                    int8_t* y_ds, hipStream_t s) {
+  const int NI = (a.OCp / JOT) * ((a.P + JL - 1) / JL), ncu = num_cus_s2i();
+  const dim3 grid(NI < ncu ? NI : ncu), block(JNW * 64);
+  if (a.out_kind == 2) {
+    if (w_ds) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 2, false>), grid, block, 0, s, a, nullptr, nullptr, nullptr,
+                       nullptr);
+  } else if (w_ds) {
+    hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true>), grid, block, 0, s, a, w_ds, al_ds, be_ds, y_ds);
+  } else {
+    hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, false>), grid, block, 0, s, a, nullptr, nullptr, nullptr,
+                       nullptr);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// Same shapes and packed weight images as conv3x3s2.hip (conv3x3w_pack for
+// conv1, downsample_pack for the 1x1).
+hipError_t launch_conv3x3s2i(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, const float* be_ds,
+                             int8_t* y_ds, hipStream_t s) {
+  if (a.OCp != a.OC || a.OC != 2 * a.C || a.H != a.W || a.OW * 2 != a.W) return hipErrorInvalidValue;
+  switch (a.W) {
+    case 56: return a.C == 64 ? launch_j<28, 64>(a, w_ds, al_ds, be_ds, y_ds, s) : hipErrorInvalidValue;
+    case 28: return a.C == 128 ? launch_j<14, 128>(a, w_ds, al_ds, be_ds, y_ds, s) : hipErrorInvalidValue;
+    case 14: return a.C == 256 ? launch_j<7, 256>(a, w_ds, al_ds, be_ds, y_ds, s) : hipErrorInvalidValue;
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace dlq

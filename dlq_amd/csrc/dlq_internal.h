@@ -54,6 +54,9 @@ size_t downsample_packed_bytes(int OC, int C);
 void downsample_pack(const int8_t* q_oc_ic, int OC, int IC, int C, int8_t* out);
 hipError_t launch_conv3x3s2(const ConvArgs& a, const int8_t* w_ds, const float* alpha_ds, const float* beta_ds,
                             int8_t* y_ds, hipStream_t s);
+// Same shapes and weight images, 196-px items (conv3x3s2i.hip).
+hipError_t launch_conv3x3s2i(const ConvArgs& a, const int8_t* w_ds, const float* alpha_ds, const float* beta_ds,
+                             int8_t* y_ds, hipStream_t s);
 // Fused layer1 basic block (block_l1.hip): C == OC == 64 at 56x56, identity
 // skip; generic packed weights of both convs.
 bool block_l1_shape(int C, int OC, int H, int W);
