@@ -57,7 +57,6 @@ __device__ unsigned long long g_stamps_i[256 * 8 * 64];
 #endif
 
 constexpr int IL = 392;        // output pixels per item
-constexpr int INT = 13;        // MFMA pixel tiles per item (416 >= 392)
 constexpr int ISC = 32;        // input channels per stage
 constexpr int IPITCH = 9 * ISC + 16;  // weight row pitch (304 B, odd multiple of 16: conflict-free)
 constexpr int INW = 8;         // waves per workgroup
@@ -215,7 +214,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       wait_vm_const<STORES>();
     else
       wait_vm_const<0>();
-    __builtin_amdgcn_s_barrier();
+    if (!(a.dbg & 16)) __builtin_amdgcn_s_barrier();  // dbg 16: timing experiment only (races)
     ISTAMP(1 + 2 * s);
     const bool more = s + 1 < nst;
     if (more && loader) prep_for(s + 1);
@@ -251,6 +250,12 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int bu = tap & 1;
+      if (a.dbg & 4) {  // timing experiment: alternate the SIMD pair's priority per tap
+        if ((tap + (wave >> 2)) & 1)
+          __builtin_amdgcn_s_setprio(1);
+        else
+          __builtin_amdgcn_s_setprio(0);
+      }
       if (tap + 1 < 9) fa[bu ^ 1] = *(const v4i*)(abase + (tap + 1) * 32);
       const int k0 = tap * DPW / 9, k1 = (tap + 1) * DPW / 9;
       if (dma) {
@@ -290,6 +295,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       }
     }
 
+    if (a.dbg & 4) __builtin_amdgcn_s_setprio(0);
     ISTAMP(2 + 2 * s);
     if (j != NS - 1) continue;
     // ---- fused epilogue of the item ----

@@ -89,6 +89,10 @@ _SIGS = {
     "dlq_mlp_destroy": ([_vp], None),
     "dlq_mlp_forward": ([_vp, _vp, _i, _vp, _vp], _i),
     "dlq_mlp_copy_hidden": ([_vp, _i, _vp, _sz, _vp], _i),
+    "dlq_preprocess_size": ([_i, _i, C.POINTER(_i), C.POINTER(_i)], _i),
+    "dlq_preprocess_u8": ([_vp, _i, _i, _i, _vp, _vp], _i),
+    "dlq_softmax_f32": ([_vp, _i, _i, _vp, _vp], _i),
+    "dlq_top1_f32": ([_vp, _i, _i, _vp, _vp, _vp], _i),
 }
 
 if not os.path.exists(LIB_PATH):

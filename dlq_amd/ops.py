@@ -229,3 +229,41 @@ def im2col_nchw_s8(x: torch.Tensor, k: int, stride: int, pad: int) -> torch.Tens
     check(lib.dlq_im2col_nchw_s8(ptr(x), N, Cc, H, W, k, k, stride, stride, pad, pad, ptr(col),
                                  stream_handle()), "im2col")
     return col
+
+
+# ------------------------------------------------------------ the path's ends
+
+def preprocess_u8(img: torch.Tensor) -> torch.Tensor:
+    """u8 RGB images [N,H,W,3] (HWC, as np.array(PIL image)) on the device ->
+    fp32 [N,3,224,224]: resize shorter side 256 (Pillow BILINEAR, bit-exact),
+    centre crop 224, normalise (RK/tools/preprocess_to_bin.py:8-33)."""
+    if not (img.is_cuda and img.dtype == torch.uint8 and img.dim() == 4 and img.shape[3] == 3):
+        raise TypeError("img must be a CUDA uint8 [N,H,W,3] tensor")
+    img = img.contiguous()
+    N, H, W, _ = img.shape
+    out = torch.empty((N, 3, 224, 224), dtype=torch.float32, device=img.device)
+    check(lib.dlq_preprocess_u8(ptr(img), N, H, W, ptr(out), stream_handle()), "preprocess_u8")
+    return out
+
+
+def preprocess_size(H: int, W: int):
+    nh, nw = C.c_int(), C.c_int()
+    check(lib.dlq_preprocess_size(H, W, C.byref(nh), C.byref(nw)), "preprocess_size")
+    return nh.value, nw.value
+
+
+def softmax(x: torch.Tensor) -> torch.Tensor:
+    """softmax_1d (RK/kernels/softmax.cu:5-47) on each row of fp32 [N,K]."""
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    check(lib.dlq_softmax_f32(ptr(x), x.shape[0], x.shape[1], ptr(y), stream_handle()), "softmax")
+    return y
+
+
+def top1(x: torch.Tensor):
+    """The launcher's top-1 (RK/runtime/infer_e2e.cu:436-438) per row: (idx int32, logit)."""
+    x = x.contiguous()
+    idx = torch.empty(x.shape[0], dtype=torch.int32, device=x.device)
+    val = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
+    check(lib.dlq_top1_f32(ptr(x), x.shape[0], x.shape[1], ptr(idx), ptr(val), stream_handle()), "top1")
+    return idx, val

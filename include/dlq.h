@@ -330,6 +330,28 @@ int dlq_mlp_forward(dlq_mlp* m, const float* x, int B, float* logits, void* stre
  * to device, async on `stream`); cap = bytes available at dst. */
 int dlq_mlp_copy_hidden(const dlq_mlp* m, int B, int8_t* dst, size_t cap, void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* The ends of the path: preprocessing and head.    */
+/* ------------------------------------------------------------------------ */
+/* Resized size of an H x W image: shorter side 256, the other
+ * round(long * 256 / short) half-to-even (RK/tools/preprocess_to_bin.py:8-16). */
+int dlq_preprocess_size(int H, int W, int* new_h, int* new_w);
+/* N u8 RGB images [N][H][W][3] (HWC, as np.array(PIL image)) -> fp32 NCHW
+ * [N][3][224][224]: Pillow BILINEAR resize of the shorter side to 256 (its
+ * 8-bit fixed-point resampler, bit-exact), centre crop 224, x/255,
+ * (x - mean)/std in fp32 (RK/tools/preprocess_to_bin.py:5-33; the input the
+ * reference uploads at RK/runtime/infer_e2e.cu:255-256).  Downscale factor
+ * at most 7. */
+int dlq_preprocess_u8(const uint8_t* img, int N, int H, int W, float* out, void* stream);
+/* softmax_1d (RK/kernels/softmax.cu:5-47) on each of N rows of K logits
+ * (expf and IEEE division: within (2e-6 + 2e-7 |x - max|) relative of an
+ * exact softmax). */
+int dlq_softmax_f32(const float* x, int N, int K, float* y, void* stream);
+/* Top-1 per row as the launcher prints it (RK/runtime/infer_e2e.cu:436-438):
+ * the first index whose logit beats the running best (initially -1e30);
+ * idx = -1 if none does.  val may be NULL. */
+int dlq_top1_f32(const float* x, int N, int K, int* idx, float* val, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -330,3 +330,107 @@ def resnet18_forward_s8(sd, scales, x, eps=1e-5):
     dumps["fc.acc"] = accs
     dumps["logits"] = logits
     return logits, dumps
+
+
+# ------------------------------------------------------------------ the ends
+# Preprocessing (RK/tools/preprocess_to_bin.py:5-33) and the head
+# (RK/kernels/softmax.cu:5-47, launcher top-1 RK/runtime/infer_e2e.cu:436-438).
+# The resize restates Pillow's 8-bit BILINEAR resampler (Pillow Resample.c:
+# precompute_coeffs, normalize_coeffs_8bpc, ImagingResample{Horizontal,
+# Vertical}_8bpc) -- the third-party algorithm under the reference's
+# Image.resize call; pinned by tests/golden/preprocess_golden.npz, written by
+# tools/make_preprocess_golden.py from the reference's own functions + PIL.
+
+PREPROC_MEAN = np.array([0.485, 0.456, 0.406], dtype=np.float32)
+PREPROC_STD = np.array([0.229, 0.224, 0.225], dtype=np.float32)
+_PREC = 22  # Resample.c PRECISION_BITS = 32 - 8 - 2
+
+
+def preprocess_size(h, w, size=256):
+    """resize_shorter_side's target (preprocess_to_bin.py:8-16): Python round."""
+    if w < h:
+        return int(round(h * size / w)), size
+    return size, int(round(w * size / h))
+
+
+def _bilinear_coeffs(in_size, out_size):
+    """precompute_coeffs (box (0, in_size), support 1) + normalize_coeffs_8bpc:
+    per output index (first source index, int32 fixed-point weights)."""
+    scale = in_size / out_size
+    filterscale = max(scale, 1.0)
+    support = 1.0 * filterscale
+    out = []
+    for xx in range(out_size):
+        center = (xx + 0.5) * scale
+        ss = 1.0 / filterscale
+        xmin = max(int(center - support + 0.5), 0)
+        xmax = min(int(center + support + 0.5), in_size) - xmin
+        w = []
+        for x in range(xmax):
+            t = abs((x + xmin - center + 0.5) * ss)
+            w.append(1.0 - t if t < 1.0 else 0.0)
+        ww = 0.0
+        for f in w:  # left-to-right double sum, as the C loop
+            ww += f
+        k = [(f / ww if ww != 0.0 else f) for f in w]
+        kk = np.array([int(-0.5 + v * (1 << _PREC)) if v < 0 else int(0.5 + v * (1 << _PREC)) for v in k],
+                      dtype=np.int64)
+        out.append((xmin, kk))
+    return out
+
+
+def _clip8(v):
+    return np.where(v >= (1 << _PREC) << 8, 255, np.where(v <= 0, 0, v >> _PREC)).astype(np.uint8)
+
+
+def _resample_axis(img, out_size, axis):
+    """One 8bpc pass along `axis` (1 = horizontal, 0 = vertical) of an HxWx3 u8 image."""
+    coeffs = _bilinear_coeffs(img.shape[axis], out_size)
+    src = np.moveaxis(img.astype(np.int64), axis, 0)
+    res = np.empty((out_size,) + src.shape[1:], dtype=np.uint8)
+    for xx, (xmin, kk) in enumerate(coeffs):
+        acc = np.full(src.shape[1:], 1 << (_PREC - 1), dtype=np.int64)
+        for i, k in enumerate(kk):
+            acc += src[xmin + i] * k
+        res[xx] = _clip8(acc)
+    return np.ascontiguousarray(np.moveaxis(res, 0, axis))
+
+
+def preprocess_resize_crop_u8(img, size=256, crop=224):
+    """Image.resize((new_w, new_h), BILINEAR) then center_crop -> u8 HxWx3."""
+    h, w = img.shape[:2]
+    nh, nw = preprocess_size(h, w, size)
+    x = img
+    if nw != w:  # Resample.c: horizontal pass first
+        x = _resample_axis(x, nw, 1)
+    if nh != h:
+        x = _resample_axis(x, nh, 0)
+    top, left = (nh - crop) // 2, (nw - crop) // 2
+    return np.ascontiguousarray(x[top:top + crop, left:left + crop])
+
+
+def preprocess_u8(img):
+    """u8 HWC RGB -> fp32 [3,224,224] (to_nchw_float32, preprocess_to_bin.py:24-33)."""
+    x = preprocess_resize_crop_u8(img).astype(np.float32) / np.float32(255.0)
+    x = (x - PREPROC_MEAN) / PREPROC_STD
+    return np.ascontiguousarray(np.transpose(x, (2, 0, 1)))
+
+
+def softmax_f64(x):
+    """Exact-as-float64 softmax of each row (the tolerance anchor for softmax_1d)."""
+    z = x.astype(np.float64) - x.astype(np.float64).max(axis=-1, keepdims=True)
+    e = np.exp(z)
+    return e / e.sum(axis=-1, keepdims=True)
+
+
+def top1(x):
+    """infer_e2e.cu:436-438: first index with logit > running best (from -1e30)."""
+    idx = np.full(x.shape[0], -1, dtype=np.int32)
+    val = np.full(x.shape[0], np.float32(-1e30), dtype=np.float32)
+    for r in range(x.shape[0]):
+        best, top = np.float32(-1e30), -1
+        for i, v in enumerate(x[r]):
+            if v > best:
+                best, top = v, i
+        idx[r], val[r] = top, best
+    return idx, val

@@ -46,3 +46,27 @@ def model_and_scales(seed=0x20260306, n_calib=2):
     torch.manual_seed(0)
     scales = calibrate_resnet18(sd, synthetic_images(n_calib, seed=seed + 1), device="cpu")
     return sd, scales
+
+
+def synth_image(h, w, seed):
+    """Seeded smooth + noisy u8 HWC RGB image (tools/make_preprocess_golden.py
+    generated the preprocessing goldens from exactly these)."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    img = np.empty((h, w, 3), np.float64)
+    for c in range(3):
+        a, b, f = rng.random(3)
+        img[..., c] = 128 + 90 * np.sin(xx * (0.02 + 0.2 * a) + yy * (0.03 + 0.1 * b) + 6 * f)
+    img += rng.normal(0, 12, size=img.shape)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+def preprocess_cases():
+    """(h, w, seed, crop_sha256, fp32_sha256) of tests/golden/preprocess_golden.npz."""
+    g = np.load(os.path.join(GOLDEN, "preprocess_golden.npz"))
+    out, i = [], 0
+    while f"case{i}_hws" in g:
+        h, w, seed = (int(v) for v in g[f"case{i}_hws"])
+        out.append((h, w, seed, g[f"case{i}_crop_sha256"].tobytes(), g[f"case{i}_sha256"].tobytes()))
+        i += 1
+    return out
