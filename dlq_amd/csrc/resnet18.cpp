@@ -12,11 +12,14 @@
 // inside forward (the reference frees temporaries per layer and syncs at
 // :280, :292, :423); the batch dimension is honoured; BN, ReLU, residual add
 // and requantisation run in the conv kernel's epilogue.
+#include <cerrno>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <iterator>
+#include <sys/stat.h>
 #include <map>
 #include <memory>
 #include <sstream>
@@ -52,8 +55,14 @@ struct Block {
 
 }  // namespace
 
+struct QTensor {  // pre-quantised weight (int8 manifest): per-output-channel int8 + scales
+  std::vector<int8_t> q;
+  std::vector<float> scale;
+};
+
 struct dlq_resnet18 {
   std::map<std::string, std::vector<float>> tensors;
+  std::map<std::string, QTensor> qtensors;
   std::map<std::string, float> scales;
   std::vector<ConvLayer> convs;
   std::vector<Block> blocks;
@@ -317,9 +326,32 @@ int record_stage(dlq_resnet18* m, const char* name, const int8_t* p, size_t byte
   return DLQ_OK;
 }
 
+// Output channels of a weight tensor (conv or fc), 0 if `name` is not one.
+int weight_oc(const dlq_resnet18* m, const std::string& name) {
+  for (const auto& c : m->convs)
+    if (name == c.wname) return c.OC;
+  return name == "fc.weight" ? 1000 : 0;
+}
+
+// The int8 weights + per-channel scales of a weight tensor: as set
+// pre-quantised (int8 manifest), or quantised now from fp32 (same function,
+// so both routes give the same bytes).
+void weights_s8(const dlq_resnet18* m, const std::string& name, int OC, int K, std::vector<int8_t>& q,
+                std::vector<float>& sw) {
+  auto it = m->qtensors.find(name);
+  if (it != m->qtensors.end()) {
+    q = it->second.q;
+    sw = it->second.scale;
+    return;
+  }
+  q.resize((size_t)OC * K);
+  sw.resize(OC);
+  quantize_weights(m->tensors.at(name).data(), OC, K, q.data(), sw.data());
+}
+
 int check_ready(const dlq_resnet18* m) {
   for (const auto& n : required_tensors(m))
-    if (!m->tensors.count(n)) return fail(DLQ_ERR_STATE, "missing tensor: " + n);
+    if (!m->tensors.count(n) && !m->qtensors.count(n)) return fail(DLQ_ERR_STATE, "missing tensor: " + n);
   std::vector<std::string> sites = {"input", "gap"};
   for (const auto& c : m->convs) sites.push_back(c.site);
   for (const auto& s : sites)
@@ -327,6 +359,48 @@ int check_ready(const dlq_resnet18* m) {
   return DLQ_OK;
 }
 
+}  // namespace
+
+namespace {
+// Whole file -> bytes (load_bin_f32, RK/include/utils.hpp:48-60, for any element type).
+int read_file(const std::string& path, std::vector<char>& out) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return fail(DLQ_ERR_IO, "open fail: " + path);
+  f.seekg(0, std::ios::end);
+  const size_t bytes = (size_t)f.tellg();
+  f.seekg(0);
+  out.resize(bytes);
+  if (bytes) f.read(out.data(), (std::streamsize)bytes);
+  if (!f) return fail(DLQ_ERR_IO, "read fail: " + path);
+  return DLQ_OK;
+}
+
+int write_file(const std::string& path, const void* p, size_t bytes) {
+  std::ofstream f(path, std::ios::binary);
+  if (!f) return fail(DLQ_ERR_IO, "open fail: " + path);
+  if (bytes) f.write((const char*)p, (std::streamsize)bytes);
+  if (!f) return fail(DLQ_ERR_IO, "write fail: " + path);
+  return DLQ_OK;
+}
+
+// manifest.json's "dtype" (the reference writes "fp32", export_resnet18.py:68-72);
+// "fp32" when there is no manifest.json (a bare directory of .bin files).
+std::string manifest_dtype(const std::string& dir) {
+  std::ifstream f(dir + "/manifest.json");
+  if (!f) return "fp32";
+  const std::string s((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  const size_t k = s.find("\"dtype\"");
+  if (k == std::string::npos) return "fp32";
+  const size_t a = s.find('"', s.find(':', k) + 1), b = a == std::string::npos ? a : s.find('"', a + 1);
+  return (a == std::string::npos || b == std::string::npos) ? "fp32" : s.substr(a + 1, b - a - 1);
+}
+
+std::vector<int> tensor_shape(const dlq_resnet18* m, const std::string& name) {
+  for (const auto& c : m->convs)
+    if (name == c.wname) return {c.OC, c.IC, c.k, c.k};
+  if (name == "fc.weight") return {1000, 512};
+  return {(int)expected_numel(m, name)};
+}
 }  // namespace
 
 extern "C" {
@@ -361,6 +435,27 @@ int dlq_resnet18_set_tensor(dlq_resnet18* m, const char* name, const float* data
     return fail(DLQ_ERR_ARG, std::string("set_tensor: ") + name + " has " + std::to_string(n) +
                                  " elements, expected " + std::to_string(want));
   m->tensors[name].assign(data, data + n);
+  m->qtensors.erase(name);
+  m->prepared = false;
+  return DLQ_OK;
+}
+
+int dlq_resnet18_set_tensor_s8(dlq_resnet18* m, const char* name, const int8_t* q, size_t n, const float* scale,
+                               size_t n_scale) {
+  if (!m || !name || !q || !scale) return fail(DLQ_ERR_ARG, "set_tensor_s8: null argument");
+  const int oc = weight_oc(m, name);
+  if (!oc) return fail(DLQ_ERR_ARG, std::string("set_tensor_s8: not a conv / fc weight: ") + name);
+  if (n != expected_numel(m, name) || n_scale != (size_t)oc)
+    return fail(DLQ_ERR_ARG, std::string("set_tensor_s8: ") + name + ": wrong element or scale count");
+  for (size_t i = 0; i < n; ++i)
+    if (q[i] == -128) return fail(DLQ_ERR_ARG, std::string("set_tensor_s8: ") + name + ": -128 (range is +-127)");
+  for (size_t o = 0; o < n_scale; ++o)
+    if (!(scale[o] > 0.f) || !std::isfinite(scale[o]))
+      return fail(DLQ_ERR_ARG, std::string("set_tensor_s8: ") + name + ": scales must be finite and > 0");
+  QTensor& t = m->qtensors[name];
+  t.q.assign(q, q + n);
+  t.scale.assign(scale, scale + n_scale);
+  m->tensors.erase(name);
   m->prepared = false;
   return DLQ_OK;
 }
@@ -374,23 +469,92 @@ int dlq_resnet18_set_scale(dlq_resnet18* m, const char* name, float scale) {
 }
 
 // load_bin_f32 (utils.hpp:48-60) without the exit(): <dir>/<name>.bin.
+
 int dlq_resnet18_load_manifest(dlq_resnet18* m, const char* dir) {
   if (!m || !dir) return fail(DLQ_ERR_ARG, "load_manifest: null argument");
+  const std::string dtype = manifest_dtype(dir);
+  if (dtype != "fp32" && dtype != "int8") return fail(DLQ_ERR_IO, "load_manifest: unsupported dtype " + dtype);
   for (const auto& n : required_tensors(m)) {
     const std::string path = std::string(dir) + "/" + n + ".bin";
-    std::ifstream f(path, std::ios::binary);
-    if (!f) return fail(DLQ_ERR_IO, "open fail: " + path);
-    f.seekg(0, std::ios::end);
-    const size_t bytes = (size_t)f.tellg();
-    f.seekg(0);
-    if (bytes % 4) return fail(DLQ_ERR_IO, "size not float-aligned: " + path);
-    std::vector<float> v(bytes / 4);
-    if (bytes) f.read((char*)v.data(), (std::streamsize)bytes);
-    if (!f) return fail(DLQ_ERR_IO, "read fail: " + path);
-    int rc = dlq_resnet18_set_tensor(m, n.c_str(), v.data(), v.size());
+    std::vector<char> raw;
+    int rc = read_file(path, raw);
+    if (rc) return rc;
+    if (dtype == "int8" && weight_oc(m, n)) {  // int8 weights + <name>.scale.bin (fp32 per output channel)
+      std::vector<char> sc;
+      if ((rc = read_file(std::string(dir) + "/" + n + ".scale.bin", sc))) return rc;
+      if (sc.size() % 4) return fail(DLQ_ERR_IO, "size not float-aligned: " + n + ".scale.bin");
+      rc = dlq_resnet18_set_tensor_s8(m, n.c_str(), (const int8_t*)raw.data(), raw.size(), (const float*)sc.data(),
+                                      sc.size() / 4);
+    } else {
+      if (raw.size() % 4) return fail(DLQ_ERR_IO, "size not float-aligned: " + path);
+      std::vector<float> v(raw.size() / 4);
+      if (!raw.empty()) std::memcpy(v.data(), raw.data(), raw.size());
+      rc = dlq_resnet18_set_tensor(m, n.c_str(), v.data(), v.size());
+    }
     if (rc) return rc;
   }
   return DLQ_OK;
+}
+
+int dlq_resnet18_save_manifest(const dlq_resnet18* m, const char* dir, int int8) {
+  if (!m || !dir) return fail(DLQ_ERR_ARG, "save_manifest: null argument");
+  for (const auto& n : required_tensors(m)) {
+    const bool w = weight_oc(m, n) != 0;
+    if (!m->tensors.count(n) && !(w && m->qtensors.count(n)))
+      return fail(DLQ_ERR_STATE, "save_manifest: missing tensor " + n);
+    if (!int8 && !m->tensors.count(n))
+      return fail(DLQ_ERR_STATE, "save_manifest: " + n + " is only held as int8; save it with int8 = 1");
+  }
+  if (mkdir(dir, 0755) != 0 && errno != EEXIST) return fail(DLQ_ERR_IO, std::string("mkdir fail: ") + dir);
+  std::ostringstream js;
+  js << "{\n  \"model\": \"resnet18\",\n  \"dtype\": \"" << (int8 ? "int8" : "fp32")
+     << "\",\n  \"layout\": \"NCHW\",\n  \"version\": 1,\n"
+     << "  \"preprocess\": {\"resize\": 256, \"center_crop\": 224, \"mean\": [0.485, 0.456, 0.406], "
+        "\"std\": [0.229, 0.224, 0.225]},\n  \"tensors\": {";
+  bool first = true;
+  for (const auto& n : required_tensors(m)) {
+    const int oc = weight_oc(m, n);
+    const std::vector<int> shape = tensor_shape(m, n);
+    int rc;
+    std::string kind, layout, extra;
+    if (oc && shape.size() == 4) kind = "conv_weight", layout = "OIHW";
+    else if (oc) kind = "fc_weight", layout = "OI";
+    else if (n.find("running_") != std::string::npos) kind = "bn_buffer", layout = "O";
+    else if (n == "fc.bias") kind = "fc_bias", layout = "O";
+    else kind = "bn_param", layout = "O";
+    if (int8 && oc) {
+      const int K = (int)(expected_numel(m, n) / oc);
+      std::vector<int8_t> q;
+      std::vector<float> sw;
+      weights_s8(m, n, oc, K, q, sw);
+      if ((rc = write_file(std::string(dir) + "/" + n + ".bin", q.data(), q.size())) ||
+          (rc = write_file(std::string(dir) + "/" + n + ".scale.bin", sw.data(), sw.size() * 4)))
+        return rc;
+      extra = ", \"dtype\": \"int8\", \"quant\": \"symmetric_per_out_channel\", \"scale_path\": \"" + n +
+              ".scale.bin\"";
+    } else {
+      const std::vector<float>& v = m->tensors.at(n);
+      if ((rc = write_file(std::string(dir) + "/" + n + ".bin", v.data(), v.size() * 4))) return rc;
+    }
+    js << (first ? "\n" : ",\n") << "    \"" << n << "\": {\"shape\": [";
+    for (size_t i = 0; i < shape.size(); ++i) js << (i ? ", " : "") << shape[i];
+    js << "], \"layout\": \"" << layout << "\", \"kind\": \"" << kind << "\", \"path\": \"" << n << ".bin\"" << extra
+       << "}";
+    first = false;
+  }
+  js << "\n  }\n}\n";
+  const std::string j = js.str();
+  return write_file(std::string(dir) + "/manifest.json", j.data(), j.size());
+}
+
+int dlq_resnet18_save_scales(const dlq_resnet18* m, const char* path) {
+  if (!m || !path) return fail(DLQ_ERR_ARG, "save_scales: null argument");
+  std::ostringstream o;
+  o << "# activation scales (site scale), dlq_resnet18_load_scales format\n";
+  o.precision(9);
+  for (const auto& kv : m->scales) o << kv.first << " " << kv.second << "\n";
+  const std::string t = o.str();
+  return write_file(path, t.data(), t.size());
 }
 
 int dlq_resnet18_load_scales(dlq_resnet18* m, const char* path) {
@@ -418,12 +582,11 @@ int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   // Weights: quantise per output channel, fold BN, pack, upload once.
   for (auto& c : m->convs) {
-    const std::vector<float>& w = m->tensors.at(c.wname);
     const int K = c.IC * c.k * c.k;
     const int ocp = packed_oc(c.OC);
-    std::vector<int8_t> q((size_t)c.OC * K);
-    std::vector<float> sw(c.OC);
-    quantize_weights(w.data(), c.OC, K, q.data(), sw.data());
+    std::vector<int8_t> q;
+    std::vector<float> sw;
+    weights_s8(m, c.wname, c.OC, K, q, sw);
     const size_t pb = packed_bytes_for(c.Cstore, c.OC, c.H, c.H, c.k, c.k, c.s, c.s, c.p, c.p);
     std::vector<int8_t> packed(pb);
     pack_conv_weights_for(c.Cstore, c.OC, c.H, c.H, c.k, c.k, c.s, c.s, c.p, c.p, q.data(), c.IC, packed.data());
@@ -459,9 +622,9 @@ int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
   }
   {  // FC: int8 [1000][512] per-row scales; logits = fmaf(acc, s_gap*s_w[o], bias[o])
     const int O = 1000, I = 512, op = packed_oc(O);
-    std::vector<int8_t> q((size_t)O * I);
-    std::vector<float> sw(O);
-    quantize_weights(m->tensors.at("fc.weight").data(), O, I, q.data(), sw.data());
+    std::vector<int8_t> q;
+    std::vector<float> sw;
+    weights_s8(m, "fc.weight", O, I, q, sw);
     std::vector<int8_t> packed(packed_bytes(O, I, 1, 1));
     pack_conv_weights(q.data(), O, I, 1, 1, I, packed.data());
     std::vector<float> alpha(op, 0.f), beta(op, 0.f);

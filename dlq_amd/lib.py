@@ -89,6 +89,9 @@ _SIGS = {
     "dlq_mlp_destroy": ([_vp], None),
     "dlq_mlp_forward": ([_vp, _vp, _i, _vp, _vp], _i),
     "dlq_mlp_copy_hidden": ([_vp, _i, _vp, _sz, _vp], _i),
+    "dlq_resnet18_set_tensor_s8": ([_vp, C.c_char_p, _vp, _sz, _vp, _sz], _i),
+    "dlq_resnet18_save_manifest": ([_vp, C.c_char_p, _i], _i),
+    "dlq_resnet18_save_scales": ([_vp, C.c_char_p], _i),
     "dlq_preprocess_size": ([_i, _i, C.POINTER(_i), C.POINTER(_i)], _i),
     "dlq_preprocess_u8": ([_vp, _i, _i, _i, _vp, _vp], _i),
     "dlq_softmax_f32": ([_vp, _i, _i, _vp, _vp], _i),

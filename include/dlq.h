@@ -269,6 +269,20 @@ int dlq_resnet18_set_scale(dlq_resnet18* m, const char* name, float scale);
 /* Read every tensor from <dir>/<name>.bin (the reference's manifest dir,
  * RK/runtime/infer_e2e.cu:262-334,428-429). */
 int dlq_resnet18_load_manifest(dlq_resnet18* m, const char* dir);
+/* Pre-quantised weight of a conv / fc layer (int8 manifest): int8 [n] in the
+ * fp32 tensor's layout, per-output-channel scales [n_scale = OC], values in
+ * +-127.  Replaces the fp32 copy; prepare then skips quantisation (the same
+ * bytes as quantising the fp32 weight with dlq_quantize_weights_s8). */
+int dlq_resnet18_set_tensor_s8(dlq_resnet18* m, const char* name, const int8_t* q, size_t n, const float* scale,
+                               size_t n_scale);
+/* Write the model's tensors as a manifest directory in the reference's
+ * export format (tools/export_resnet18.py:57-113: <name>.bin raw tensors +
+ * manifest.json with shape / layout / kind / path).  int8 = 1: conv and fc
+ * weights as int8 <name>.bin + fp32 <name>.scale.bin, "dtype": "int8"
+ * (dlq_resnet18_load_manifest reads both kinds). */
+int dlq_resnet18_save_manifest(const dlq_resnet18* m, const char* dir, int int8);
+/* Write the activation scales in dlq_resnet18_load_scales' text format. */
+int dlq_resnet18_save_scales(const dlq_resnet18* m, const char* path);
 /* Read "<site> <scale>" lines (the int8 quant block). */
 int dlq_resnet18_load_scales(dlq_resnet18* m, const char* path);
 /* Quantise + fold + upload weights, allocate the workspace for up to
