@@ -132,8 +132,14 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   // offset (weights: byte offset into a.w; patch: into a.x, -1 = zero unit).
   int doff[DPW];
   int iss_li = -1;
+  // CUs of one XCD start their piece sequence at different pieces, so they do
+  // not all request the same weight lines of the shared L2 at once (measured
+  // 1-3 % faster than every CU issuing in the same order)
+  const int rot = (int)((blockIdx.x >> 3) % DPW);
   auto piece_of = [&](int k) {
-    const int pc = lrank + k * NLD;
+    int kk = k + rot;
+    kk = kk >= DPW ? kk - DPW : kk;
+    const int pc = lrank + kk * NLD;
     return pc >= G::NPIECE ? pc - G::NPIECE : pc;  // past the end: re-issue an earlier piece
   };
   auto prep_issue = [&](int li) {
@@ -342,13 +348,11 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
         unsigned q[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] = __builtin_fmaf((float)acc[f][4 * g + e], al[g][e], be[g][e]);
-            if constexpr (RES) v[e] = __builtin_fmaf((float)(int)(signed char)(rg[g] >> (8 * e)), a.s_res, v[e]);
-          }
-          q[g] = quant4(v[0], v[1], v[2], v[3], lo);
+          const int ac[4] = {acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
+          if constexpr (RES)
+            q[g] = epi4_res(ac, al[g], be[g], rg[g], a.s_res, lo);
+          else
+            q[g] = epi4(ac, al[g], be[g], lo);
         }
         swap32(q[0], q[2]);
         swap32(q[1], q[3]);

@@ -88,8 +88,11 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
   // ---- DMA issue side (pieces pc = wave + 8k): conv weights, ds weights, patch
   int doff[DPW];
   int iss_li = -1;
+  const int rot = (int)((blockIdx.x >> 3) % DPW);  // stagger the XCD's CUs over the shared weight lines
   auto piece_of = [&](int k) {
-    const int pc = wave + k * JNW;
+    int kk = k + rot;
+    kk = kk >= DPW ? kk - DPW : kk;
+    const int pc = wave + kk * JNW;
     return pc >= G::NPIECE ? pc - G::NPIECE : pc;
   };
   auto prep_issue = [&](int li) {
@@ -206,7 +209,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
         if (tap == 3) fd = *(const v4i*)(lds + sb + d_row);  // the downsample's A fragment, used at tap 4
       }
       const int k0 = tap * DPW / 9, k1 = (tap + 1) * DPW / 9;
-      if (more) {
+      if (more && !(a.dbg & 2)) {  // dbg 2: timing experiment without the DMA
 #pragma unroll
         for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
       }
@@ -274,10 +277,8 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
           unsigned q[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf((float)ac[f][4 * g + e], al[g][e], be[g][e]);
-            q[g] = quant4(v[0], v[1], v[2], v[3], lo);
+            const int a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
+            q[g] = epi4(a4, al[g], be[g], lo);
           }
           swap32(q[0], q[2]);
           swap32(q[1], q[3]);

@@ -39,6 +39,40 @@ __device__ __forceinline__ unsigned quant4(float y0, float y1, float y2, float y
   return __builtin_amdgcn_perm(u1, u0, 0x0c0c0400u) | __builtin_amdgcn_perm(u3, u2, 0x04000c0cu);
 }
 
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+// Fused epilogue of 4 accumulators (one MFMA-layout register group):
+// y = fma(float(acc), alpha, beta) [+ fma(float(res byte), r_s, y)], then
+// quant4.  The fmas and the rounding add run as packed FP32 pairs
+// (v_pk_fma_f32 / v_pk_add_f32: the same IEEE operations per element, so
+// bit-identical to the scalar sequence and to oracle.c).
+__device__ __forceinline__ unsigned epi4(const int* acc, const float* al, const float* be, float lo) {
+  const v2f y01 = __builtin_elementwise_fma(v2f{(float)acc[0], (float)acc[1]}, v2f{al[0], al[1]}, v2f{be[0], be[1]});
+  const v2f y23 = __builtin_elementwise_fma(v2f{(float)acc[2], (float)acc[3]}, v2f{al[2], al[3]}, v2f{be[2], be[3]});
+  v2f c01 = {__builtin_amdgcn_fmed3f(y01[0], lo, 127.f), __builtin_amdgcn_fmed3f(y01[1], lo, 127.f)};
+  v2f c23 = {__builtin_amdgcn_fmed3f(y23[0], lo, 127.f), __builtin_amdgcn_fmed3f(y23[1], lo, 127.f)};
+  const v2f M = {12582912.0f, 12582912.0f};
+  c01 = c01 + M;
+  c23 = c23 + M;
+  return __builtin_amdgcn_perm(__float_as_uint(c01[1]), __float_as_uint(c01[0]), 0x0c0c0400u) |
+         __builtin_amdgcn_perm(__float_as_uint(c23[1]), __float_as_uint(c23[0]), 0x04000c0cu);
+}
+__device__ __forceinline__ unsigned epi4_res(const int* acc, const float* al, const float* be, unsigned r4, float r_s,
+                                             float lo) {
+  const v2f s = {r_s, r_s};
+  v2f y01 = __builtin_elementwise_fma(v2f{(float)acc[0], (float)acc[1]}, v2f{al[0], al[1]}, v2f{be[0], be[1]});
+  v2f y23 = __builtin_elementwise_fma(v2f{(float)acc[2], (float)acc[3]}, v2f{al[2], al[3]}, v2f{be[2], be[3]});
+  y01 = __builtin_elementwise_fma(v2f{(float)(int)(signed char)r4, (float)(int)(signed char)(r4 >> 8)}, s, y01);
+  y23 = __builtin_elementwise_fma(v2f{(float)(int)(signed char)(r4 >> 16), (float)((int)r4 >> 24)}, s, y23);
+  v2f c01 = {__builtin_amdgcn_fmed3f(y01[0], lo, 127.f), __builtin_amdgcn_fmed3f(y01[1], lo, 127.f)};
+  v2f c23 = {__builtin_amdgcn_fmed3f(y23[0], lo, 127.f), __builtin_amdgcn_fmed3f(y23[1], lo, 127.f)};
+  const v2f M = {12582912.0f, 12582912.0f};
+  c01 = c01 + M;
+  c23 = c23 + M;
+  return __builtin_amdgcn_perm(__float_as_uint(c01[1]), __float_as_uint(c01[0]), 0x0c0c0400u) |
+         __builtin_amdgcn_perm(__float_as_uint(c23[1]), __float_as_uint(c23[0]), 0x04000c0cu);
+}
+
 // Bijective XCD-aware remap: consecutive logical tiles land on one XCD
 // (cdna_hip_programming.md §5 "XCD swizzle must be bijective").
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

@@ -3,8 +3,9 @@
 // gap_kernel replaces gap_global / gap_global_ref (RK = CUDA/resnet18-kernel-
 // lab/cpp/fp32: RK/kernels/gap_global.cu:2-33, RK/runtime/infer_e2e.cu:37-61)
 // on int8 NHWC: exact int32 channel sums, then clamp(rne(float(sum) * k)).
-// Each thread sums 16 channels over a quarter of the pixels with 16-byte
-// loads; the four quarters meet through two xor-shuffles.
+// Each thread sums 16 channels over an eighth of the pixels with 16-byte
+// loads (two in flight); the eight partial sums meet through three
+// xor-shuffles.
 //
 // linear_kernel replaces fc_forward (RK/runtime/infer_e2e.cu:206-219:
 // sgemm_tiled M=1000 N=1 K=512 + host bias) and the MNIST forward GEMMs
@@ -20,16 +21,26 @@ namespace {
 
 __global__ __launch_bounds__(256) void gap16_kernel(const int8_t* __restrict__ x, int N, int C, int HW, float k,
                                                     int8_t* __restrict__ y) {
-  const int tpi = (C / 16) * 4;  // threads per image
+  const int tpi = (C / 16) * 8;  // threads per image: 8 pixel groups per 16-channel group
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int n = (int)(t / tpi), r = (int)(t - (long)n * tpi);
-  const int pg = r & 3, cg = r >> 2;
+  const int pg = r & 7, cg = r >> 3;
   int s[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) s[i] = 0;
   if (n < N) {
     const int8_t* src = x + (size_t)n * HW * C + cg * 16;
-    for (int i = pg; i < HW; i += 4) {
+    int i = pg;
+    for (; i + 8 < HW; i += 16) {  // two independent 16-byte loads in flight per step
+      const v4i v0 = *(const v4i*)(src + (size_t)i * C);
+      const v4i v1 = *(const v4i*)(src + (size_t)(i + 8) * C);
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          s[w * 4 + b] += (int)(signed char)(v0[w] >> (8 * b)) + (int)(signed char)(v1[w] >> (8 * b));
+    }
+    if (i < HW) {
       const v4i v = *(const v4i*)(src + (size_t)i * C);
 #pragma unroll
       for (int w = 0; w < 4; ++w)
@@ -41,6 +52,7 @@ __global__ __launch_bounds__(256) void gap16_kernel(const int8_t* __restrict__ x
   for (int i = 0; i < 16; ++i) {
     s[i] += __shfl_xor(s[i], 1);
     s[i] += __shfl_xor(s[i], 2);
+    s[i] += __shfl_xor(s[i], 4);
   }
   if (n < N && pg == 0) {
     v4i o;
@@ -119,7 +131,7 @@ __global__ __launch_bounds__(64) void linear_kernel(const int8_t* __restrict__ x
 }  // namespace
 
 hipError_t launch_gap(const int8_t* x, int N, int C, int HW, float k, int8_t* y, hipStream_t s) {
-  const long total = (long)N * (C / 16) * 4;
+  const long total = (long)N * (C / 16) * 8;
   hipLaunchKernelGGL(gap16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, N, C, HW, k, y);
   return hipGetLastError();
 }

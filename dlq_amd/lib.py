@@ -20,8 +20,8 @@ LIB_PATH = os.path.join(_HERE, "libdlq.so")
 DLQ_OK = 0
 DLQ_OUT_S8, DLQ_OUT_F32, DLQ_OUT_S32 = 0, 1, 2
 # kernel families of dlq_resnet18_timing (include/dlq.h DLQ_FAM_*)
-FAMILIES = ["stem_fused_kernel", "block_l1_kernel (layer1 block)", "conv3x3s2_kernel (+downsample)",
-            "conv3x3w_kernel (layer2-4 s1)", "gap16_kernel", "linear_kernel (fc)", "other"]
+FAMILIES = ["stem_fused_kernel", "block_l1_kernel (layer1 block)", "conv3x3s2i_kernel (+downsample)",
+            "conv3x3i_kernel (layer2-4 s1)", "gap16_kernel", "linear_kernel (fc)", "other"]
 
 
 class DLQError(RuntimeError):

@@ -1,0 +1,53 @@
+// Timing probe (not product code): the 196-px stride-2 conv + fused
+// downsample kernel (conv3x3s2i.hip) on the three ResNet-18 shapes, random
+// int8 data, B = 256; argv: OW (28/14/7), dbg bits (2 = no LDS-DMA).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//          -I dlq_amd/csrc tools/probe/conv3x3s2i_probe.hip -o tools/probe/conv3x3s2i_probe
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+namespace dlq {
+int packed_oc(int OC) { return OC <= 64 ? 64 : (OC + 127) / 128 * 128; }
+}
+#include "../../dlq_amd/csrc/conv3x3s2i.hip"
+
+using namespace dlq;
+__global__ void fill_rand(int8_t* p, size_t n, unsigned seed) {
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    unsigned x = (unsigned)i * 2654435761u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    p[i] = (int8_t)((int)(x % 255u) - 127);
+  }
+}
+int main(int argc, char** argv) {
+  const int OW = argc > 1 ? atoi(argv[1]) : 7;
+  const int dbg = argc > 2 ? atoi(argv[2]) : 0;
+  const int C = OW == 28 ? 64 : OW == 14 ? 128 : 256, OC = 2 * C, N = 256, W = 2 * OW;
+  const size_t xin = (size_t)N * W * W * C, yout = (size_t)N * OW * OW * OC;
+  const size_t wb = (size_t)OC * (C / 32) * 304, db = (size_t)OC * (C / 32) * 48;
+  int8_t *x, *w, *wd, *y, *yd;
+  float *al, *be;
+  if (hipMalloc(&x, xin) || hipMalloc(&y, yout) || hipMalloc(&yd, yout) || hipMalloc(&w, wb) ||
+      hipMalloc(&wd, db) || hipMalloc(&al, OC * 4) || hipMalloc(&be, OC * 4)) return 3;
+  hipLaunchKernelGGL(fill_rand, dim3(1024), dim3(256), 0, 0, x, xin, 1u);
+  hipLaunchKernelGGL(fill_rand, dim3(1024), dim3(256), 0, 0, w, wb, 3u);
+  hipLaunchKernelGGL(fill_rand, dim3(1024), dim3(256), 0, 0, wd, db, 4u);
+  std::vector<float> hal(OC, 1e-4f);
+  if (hipMemcpy(al, hal.data(), OC * 4, hipMemcpyHostToDevice) || hipMemset(be, 0, OC * 4)) return 3;
+  ConvArgs a{};
+  a.x = x; a.w = w; a.alpha = al; a.beta = be; a.y = y;
+  a.N = N; a.H = W; a.W = W; a.C = C; a.OH = OW; a.OW = OW; a.OC = OC; a.OCp = OC; a.K = 9 * C;
+  a.kH = a.kW = 3; a.sH = a.sW = 2; a.pH = a.pW = 1; a.P = N * OW * OW; a.relu = 1; a.out_kind = 0; a.dbg = dbg;
+  hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+  for (int it = 0; it < 20; ++it) launch_conv3x3s2i(a, wd, al, be, yd, 0);
+  hipEventRecord(e0, 0);
+  for (int it = 0; it < 20; ++it) launch_conv3x3s2i(a, wd, al, be, yd, 0);
+  hipEventRecord(e1, 0);
+  if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    printf("launch/sync failed\n");
+    return 2;
+  }
+  float ms; hipEventElapsedTime(&ms, e0, e1);
+  printf("OW=%d dbg=%d kernel %.1f us\n", OW, dbg, ms * 1e3 / 20);
+  return 0;
+}
