@@ -101,7 +101,9 @@ __device__ __forceinline__ void wave_tiles(int wave, int& mt, int& f0, int& nf) 
 }
 
 // NLD loader waves issue the LDS-DMA, lrank = this wave's rank among them
-// (every wave: handing the DMA to the pairs' less loaded waves measured slower).
+// (every wave: handing the DMA to the pairs' less loaded waves measured
+// slower; so did alternating the pair's priority per tap, splitting the 13th
+// tile between the pair by taps, and 12 waves (3 per SIMD)).
 template <int W, int C, int OUT, bool RES, int NF, int NLD>
 __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int mt, int f0, int lrank) {
   using G = IGeo<W>;
@@ -256,12 +258,6 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int bu = tap & 1;
-      if (a.dbg & 4) {  // timing experiment: alternate the SIMD pair's priority per tap
-        if ((tap + (wave >> 2)) & 1)
-          __builtin_amdgcn_s_setprio(1);
-        else
-          __builtin_amdgcn_s_setprio(0);
-      }
       if (tap + 1 < 9) fa[bu ^ 1] = *(const v4i*)(abase + (tap + 1) * 32);
       const int k0 = tap * DPW / 9, k1 = (tap + 1) * DPW / 9;
       if (dma) {
@@ -301,7 +297,6 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       }
     }
 
-    if (a.dbg & 4) __builtin_amdgcn_s_setprio(0);
     ISTAMP(2 + 2 * s);
     if (j != NS - 1) continue;
     // ---- fused epilogue of the item ----
