@@ -210,17 +210,27 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
       hpool(conv_row(2 * py0 - 1), Hp);
     }
 
+    // The staged output of step p is read back and stored during step p+1
+    // (after its convert), so the LDS round trip and the store issue overlap
+    // the next step instead of closing this one.
+    const int pxl = lane >> 1, hf = lane & 1;
+    auto store_row = [&](int p) {
+      const v4i o = *(const v4i*)(stg + pxl * 32 + hf * 16);
+      if (lane < 28) *(v4i*)(a.y + (((size_t)n * 56 + p) * 56 + 14 * q + pxl) * 64 + ot * 32 + hf * 16) = o;
+    };
     for (int p = py0; p < py1; ++p) {
       const int t = p - py0;
       // Pair t+3 (super rows 2p+3, 2p+4) has landed once only the younger VM
-      // ops remain: pairs t+4 .. t+2+SLA and the output stores of the last
-      // min(t, SLA) steps.
+      // ops remain: pairs t+4 .. t+2+SLA and the stores issued in steps
+      // t-SLA+1 .. t-1 (each step stores the previous step's row before it
+      // issues its pair): min(t-1, SLA-1) of them.
       ST(5);
-      wait_vm((SLA - 1) * D + (t < SLA ? t : SLA));
+      wait_vm((SLA - 1) * D + (t < 1 ? 0 : (t - 1 < SLA - 1 ? t - 1 : SLA - 1)));
       __builtin_amdgcn_s_barrier();
       ST(0);
       convert_pair(t + 3);
       ST(1);
+      if (t > 0) store_row(p - 1);
       issue_pair(t + 3 + SLA);
       ST(2);
 
@@ -237,12 +247,11 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
         const unsigned u = __float_as_uint(__builtin_amdgcn_fmed3f(y, 0.f, 127.f) + 12582912.0f);
         stg[(m + 8 * lh) * 32 + lr] = (int8_t)u;
       }
-      // 14 pooled columns x 32 channels = 28 x 16 B (written by this wave: LDS is in order)
-      const int pxl = lane >> 1, hf = lane & 1;
-      const v4i o = *(const v4i*)(stg + pxl * 32 + hf * 16);
-      if (lane < 28) *(v4i*)(a.y + (((size_t)n * 56 + p) * 56 + 14 * q + pxl) * 64 + ot * 32 + hf * 16) = o;
+      // 14 pooled columns x 32 channels = 28 x 16 B, staged in LDS (written by
+      // this wave: LDS is in order); stored during the next step
       ST(4);
     }
+    if (py1 > py0) store_row(py1 - 1);
     wait_vm0();
     __syncthreads();  // ring reuse by the next item
   }
