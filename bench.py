@@ -37,6 +37,9 @@ def parse():
                     help="bounded sample for the CPU oracle baseline (0 = skip)")
     ap.add_argument("--torch-cpu-images", type=int, default=8,
                     help="images for the torch fp32 CPU reference timing (0 = skip)")
+    ap.add_argument("--precision", choices=("int8", "fp8"), default="int8",
+                    help="int8 = the headline (configs[2]/[3]); fp8 = e4m3 activations + per-channel "
+                         "e4m3 weights on the fp8 MFMA (configs[4])")
     return ap.parse_args()
 
 
@@ -83,17 +86,20 @@ def pmc_traffic(kernel_family):
         return None
 
 
-def cpu_oracle_baseline(sd, scales, n_images):
+def cpu_oracle_baseline(sd, scales, n_images, fp8=False):
     """The oracle (C restatement, 1 thread) on a bounded sample of the same workload."""
     from oracle import oracle as O
     from dlq_amd.models import synthetic_images
+    fwd = O.resnet18_forward_f8 if fp8 else O.resnet18_forward_s8
+    if fp8:
+        n_images = max(1, n_images // 2)  # exact int64 accumulation: ~2x slower per image
     x = synthetic_images(n_images, seed=SEED + 17).numpy()
-    O.resnet18_forward_s8(sd, scales, x[:1])  # warm caches / page in
+    fwd(sd, scales, x[:1])  # warm caches / page in
     t0 = time.perf_counter()
-    O.resnet18_forward_s8(sd, scales, x)
+    fwd(sd, scales, x)
     dt = time.perf_counter() - t0
     return {"value": round(n_images / dt, 3), "unit": "images/s", "cores": 1, "kind": "port",
-            "sample": f"{n_images} images 3x224x224, int8 ResNet-18 via oracle/oracle.c "
+            "sample": f"{n_images} images 3x224x224, {'fp8' if fp8 else 'int8'} ResNet-18 via oracle/oracle.c "
                       f"(single thread), {dt:.2f} s"}
 
 
@@ -126,8 +132,9 @@ def main():
     B = args.batch
     sd = resnet18_state_dict(SEED)
     # Offline calibration on the CPU (deterministic, identical on every rank).
-    scales = calibrate_resnet18(sd, synthetic_images(2, seed=SEED + 1), device="cpu")
-    model = ResNet18Int8(sd, scales, max_batch=B)
+    fp8 = args.precision == "fp8"
+    scales = calibrate_resnet18(sd, synthetic_images(2, seed=SEED + 1), device="cpu", qmax=448.0 if fp8 else 127.0)
+    model = ResNet18Int8(sd, scales, max_batch=B, precision=args.precision)
     conv_macs, fc_macs = model.macs_per_image()
 
     # Synthetic NCHW input generated on the device (seeded per rank), resident in HBM.
@@ -187,7 +194,7 @@ def main():
         ent = {"launches_per_forward": round(per_fwd, 2), "avg_launch_us": round(avg_us, 2),
                "ms_per_forward": round(fam_ms[f] / max(n_fwd, 1), 4)}
         if fam_macs[f] > 0:
-            ent["tflops_int8"] = round(2.0 * fam_macs[f] * B / per_fwd / (avg_us * 1e-6) / 1e12, 1)
+            ent["tflops_fp8" if fp8 else "tflops_int8"] = round(2.0 * fam_macs[f] * B / per_fwd / (avg_us * 1e-6) / 1e12, 1)
         if fam_bytes[f] > 0:
             ent["act_gb_s"] = round(fam_bytes[f] * B / per_fwd / (avg_us * 1e-6) / 1e9, 1)
         families[name] = ent
@@ -199,8 +206,15 @@ def main():
     achieved = ops_per_launch / (dom_avg_us * 1e-6) / 1e12 if dom_avg_us > 0 else 0.0
     traffic = pmc_traffic(FAMILIES[dom])
 
+    metric = "images/sec ResNet-18 int8 batch=256 @1/2/4/8 GPU; int8 GEMM TOPS vs peak"
+    workload = ("ResNet-18 int8 224x224, batch 256 per GPU (BASELINE configs[2]; "
+                "N>1 = configs[3] with RCCL logits all-gather)")
+    if fp8:
+        metric = "images/sec ResNet-18 fp8 (e4m3) batch=256; fp8 MFMA TFLOPS vs peak"
+        workload = ("ResNet-18 per-channel e4m3 weights + e4m3 activations on v_mfma_f32_32x32x64_f8f6f4, "
+                    "224x224, batch 256 per GPU (BASELINE configs[4])")
     out = {
-        "metric": "images/sec ResNet-18 int8 batch=256 @1/2/4/8 GPU; int8 GEMM TOPS vs peak",
+        "metric": metric,
         "value": round(value, 1),
         "unit": "images/s",
         "n_gpus": world,
@@ -210,16 +224,15 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int8",
+        "dtype": "fp8_e4m3" if fp8 else "int8",
         "data": "synthetic (seeded u8 pixels normalised; seeded random-init ResNet-18 weights, "
-                "CPU-calibrated int8 scales)",
-        "config": {"workload": "ResNet-18 int8 224x224, batch 256 per GPU (BASELINE configs[2]; "
-                               "N>1 = configs[3] with RCCL logits all-gather)",
+                f"CPU-calibrated {args.precision} scales)",
+        "config": {"workload": workload,
                    "global_batch": world * B, "per_gpu_batch": B,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         "roofline": {"bound": "mfma", "kernel": FAMILIES[dom],
                      "achieved": round(achieved, 1), "peak": round(PEAK_I8_TOPS, 1),
-                     "unit": "TFLOP/s", "int8_ops": True,
+                     "unit": "TFLOP/s", "int8_ops": not fp8,
                      "frac": round(achieved / PEAK_I8_TOPS, 4), "traffic": traffic,
                      "ops_per_launch": ops_per_launch, "avg_launch_us": round(dom_avg_us, 2),
                      "launches_timed": fam_n[dom], "timing": "hipEvents on the forward's stream around "
@@ -233,7 +246,7 @@ def main():
     if rank == 0 and world == 1:
         try:
             if args.cpu_baseline_images > 0:
-                out["cpu_baseline"] = cpu_oracle_baseline(sd, scales, args.cpu_baseline_images)
+                out["cpu_baseline"] = cpu_oracle_baseline(sd, scales, args.cpu_baseline_images, fp8)
             if args.torch_cpu_images > 0:
                 out["cpu_torch_fp32"] = torch_cpu_baseline(sd, args.torch_cpu_images)
             out["cpu_model"] = platform.processor() or platform.machine()

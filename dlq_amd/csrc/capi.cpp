@@ -243,6 +243,17 @@ int conv_args(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, c
 }
 }  // namespace
 
+}  // extern "C"
+namespace dlq {
+int conv_args_checked(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
+                      const float* beta, const int8_t* residual, float res_scale, int relu, int out_kind, void* y,
+                      ConvArgs& a) {
+  bool wide = false;
+  return conv_args(d, x, w_packed, alpha, beta, residual, res_scale, relu, out_kind, y, a, wide);
+}
+}  // namespace dlq
+extern "C" {
+
 int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
                        const float* alpha, const float* beta, const int8_t* residual,
                        float res_scale, int relu, int out_kind, void* y, void* stream) {

@@ -116,7 +116,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   const bool loader = lrank >= 0;
   constexpr int STORES = OUT == 0 ? NF : 4 * NF;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int lr = lane & 31, lh = lane >> 5;
   const int n_ot = a.OCp / G::OT;
   const int n_pi = (a.P + IL - 1) / IL;

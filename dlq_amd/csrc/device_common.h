@@ -73,6 +73,25 @@ __device__ __forceinline__ unsigned epi4_res(const int* acc, const float* al, co
          __builtin_amdgcn_perm(__float_as_uint(c23[1]), __float_as_uint(c23[0]), 0x04000c0cu);
 }
 
+// ---- fp8 (e4m3, OCP) helpers: DESIGN.md §3b, oracle.c ora_*_f8 ----------
+typedef float v16f __attribute__((ext_vector_type(16)));
+typedef int v8i __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ v8i cat8(v4i lo, v4i hi) { return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7); }
+
+// requant of 4 values to e4m3: clamp(y, lo, 448) (v_med3), -0 -> +0 (+0.0f),
+// round-to-nearest-even encode (v_cvt_pk_fp8_f32, byte j = value j).
+// Bit-identical to oracle.c f8_requant (tests/test_gpu_f8.py).
+__device__ __forceinline__ unsigned enc4_f8(float y0, float y1, float y2, float y3, float lo) {
+  const float c0 = __builtin_amdgcn_fmed3f(y0, lo, 448.f) + 0.0f;
+  const float c1 = __builtin_amdgcn_fmed3f(y1, lo, 448.f) + 0.0f;
+  const float c2 = __builtin_amdgcn_fmed3f(y2, lo, 448.f) + 0.0f;
+  const float c3 = __builtin_amdgcn_fmed3f(y3, lo, 448.f) + 0.0f;
+  int r = __builtin_amdgcn_cvt_pk_fp8_f32(c0, c1, 0, false);
+  r = __builtin_amdgcn_cvt_pk_fp8_f32(c2, c3, r, true);
+  return (unsigned)r;
+}
+
 // Bijective XCD-aware remap: consecutive logical tiles land on one XCD
 // (cdna_hip_programming.md §5 "XCD swizzle must be bijective").
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

@@ -80,6 +80,13 @@ hipError_t launch_linear(const int8_t* x, int N, int K, const int8_t* w, int OC,
 hipError_t launch_im2col_nchw(const int8_t* x, int N, int C, int H, int W, int kH, int kW, int sH,
                               int sW, int pH, int pW, int8_t* col, hipStream_t s);
 
+// fp8 (e4m3) path (kernels.hip conv_s8_kernel<..., F8>, fp8.hip): generic
+// packed layout only.
+hipError_t launch_conv_f8(const ConvArgs& a, hipStream_t s);
+uint8_t f8_encode_host(float y);
+uint8_t f8_requant_host(float y, float lo);
+void quantize_weights_f8(const float* w, int OC, int K, uint8_t* q, float* scale);
+
 // Thread-local error message (capi.cpp).
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
@@ -99,6 +106,14 @@ bool wide_layout(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, in
 size_t packed_bytes_for(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW);
 void pack_conv_weights_for(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW,
                            const int8_t* q_oihw, int IC, int8_t* packed);
+
+// Validation + ConvArgs of one conv launch (capi.cpp conv_args).
+}  // namespace dlq
+struct dlq_conv_desc;
+namespace dlq {
+int conv_args_checked(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
+                      const float* beta, const int8_t* residual, float res_scale, int relu, int out_kind, void* y,
+                      ConvArgs& a);
 
 inline int out_dim(int in, int k, int s, int p) { return (in + 2 * p - k) / s + 1; }
 

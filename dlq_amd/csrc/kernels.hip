@@ -24,6 +24,7 @@
 //   B: lane l holds X[col l&31][k 16*(l>>5) .. +15]
 //   D: reg r of lane l is D[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31]
 #include <cstdlib>
+#include <type_traits>
 
 #include "device_common.h"
 
@@ -50,8 +51,15 @@ struct TileCfg {
 //         K = 256 ordered (kh, kw, c); one K step = 2 kh rows x 8 kw x 4 c;
 //         a 16-B chunk = 4 taps of one row, loaded as 4 dwords.
 // OUT: DLQ_OUT_S8 (0), DLQ_OUT_F32 (1), DLQ_OUT_S32 (2).
-template <int TOC, int TP, int WOC, int MODE, int OUT, bool RES>
+// F8: operands are e4m3 codes (the fp8 path): the same bytes
+//     staged the same way, but each K step is ONE v_mfma_f32_32x32x64_f8f6f4
+//     (the scaled builtin with zero scales lowers to the unscaled opcode) on
+//     fp32 accumulators; lane half h feeds chunks h and 2+h of the step as
+//     bytes 0-15 / 16-31 of its 32-byte fragment, identically for A and B, so
+//     every product pairs the same k.  Epilogue enc4_f8 (OUT 0 only).
+template <int TOC, int TP, int WOC, int MODE, int OUT, bool RES, bool F8 = false>
 __global__ __launch_bounds__(NT) void conv_s8_kernel(ConvArgs a) {
+  static_assert(!F8 || OUT != 1, "fp8 convs produce e4m3 or raw fp32 accumulators");
   using T = TileCfg<TOC, TP, WOC>;
   __shared__ __attribute__((aligned(16))) int8_t lds[2 * T::BUF];
 
@@ -137,16 +145,41 @@ __global__ __launch_bounds__(NT) void conv_s8_kernel(ConvArgs a) {
     }
   };
 
-  v16i acc[T::FM][T::FN];
+  using Acc = typename std::conditional<F8, v16f, v16i>::type;
+  Acc acc[T::FM][T::FN];
 #pragma unroll
   for (int fm = 0; fm < T::FM; ++fm)
 #pragma unroll
-    for (int fn = 0; fn < T::FN; ++fn) acc[fm][fn] = v16i{0};
+    for (int fn = 0; fn < T::FN; ++fn) acc[fm][fn] = Acc{0};
 
   const int lr = lane & 31, lh = lane >> 5;
   auto compute = [&](int buf) {
     const int8_t* A = lds + buf * T::BUF;
     const int8_t* B = A + TOC * BK;
+    if constexpr (F8) {
+      v4i af[2][T::FM], bf[2][T::FN];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = 2 * kk + lh;
+#pragma unroll
+        for (int fm = 0; fm < T::FM; ++fm) {
+          const int row = wo * T::WTOC + fm * 32 + lr;
+          af[kk][fm] = *(const v4i*)(A + row * BK + swz(row, ch) * 16);
+        }
+#pragma unroll
+        for (int fn = 0; fn < T::FN; ++fn) {
+          const int row = wp * T::WTP + fn * 32 + lr;
+          bf[kk][fn] = *(const v4i*)(B + row * BK + swz(row, ch) * 16);
+        }
+      }
+#pragma unroll
+      for (int fm = 0; fm < T::FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < T::FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+              cat8(af[0][fm], af[1][fm]), cat8(bf[0][fn], bf[1][fn]), acc[fm][fn], 0, 0, 0, 0, 0, 0);
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int ch = 2 * kk + lh;
@@ -197,8 +230,9 @@ __global__ __launch_bounds__(NT) void conv_s8_kernel(ConvArgs a) {
         const int oc = ocb + 8 * g;  // this lane's 4 consecutive channels oc..oc+3
         if (oc >= OC) continue;
         const size_t o = (size_t)pix * OC + oc;
-        if constexpr (OUT == 2) {
-          int* yp = (int*)a.y + o;
+        if constexpr (OUT == 2) {  // raw accumulators: int32, or fp32 for F8
+          using E = typename std::conditional<F8, float, int>::type;
+          E* yp = (E*)a.y + o;
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             if (oc + j < OC) yp[j] = acc[fm][fn][4 * g + j];
@@ -210,7 +244,16 @@ __global__ __launch_bounds__(NT) void conv_s8_kernel(ConvArgs a) {
           float y[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) y[j] = __builtin_fmaf((float)acc[fm][fn][4 * g + j], alv[j], bev[j]);
-          if constexpr (OUT == 1) {
+          if constexpr (F8) {
+            if constexpr (RES) {
+              const int rq = *(const int*)(a.res + o);
+              y[0] = __builtin_fmaf(__builtin_amdgcn_cvt_f32_fp8(rq, 0), a.s_res, y[0]);
+              y[1] = __builtin_fmaf(__builtin_amdgcn_cvt_f32_fp8(rq, 1), a.s_res, y[1]);
+              y[2] = __builtin_fmaf(__builtin_amdgcn_cvt_f32_fp8(rq, 2), a.s_res, y[2]);
+              y[3] = __builtin_fmaf(__builtin_amdgcn_cvt_f32_fp8(rq, 3), a.s_res, y[3]);
+            }
+            *(unsigned*)((int8_t*)a.y + o) = enc4_f8(y[0], y[1], y[2], y[3], a.relu ? 0.f : -448.f);
+          } else if constexpr (OUT == 1) {
             float* yp = (float*)a.y + o;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -246,6 +289,22 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
     else return hipErrorInvalidValue;
   } else {
     hipLaunchKernelGGL((conv_s8_kernel<TOC, TP, WOC, MODE, 0, false>), grid, block, 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+// fp8 convs: the generic tiles only (generic packed layout, MODE 0 / stem).
+template <int TOC, int TP, int WOC, int MODE>
+hipError_t launch_cfg_f8(const ConvArgs& a, hipStream_t s) {
+  const int ntile = (a.OCp / TOC) * ((a.P + TP - 1) / TP);
+  const dim3 grid(ntile), block(NT);
+  if (a.out_kind == 2) {
+    hipLaunchKernelGGL((conv_s8_kernel<TOC, TP, WOC, MODE, 2, false, true>), grid, block, 0, s, a);
+  } else if (a.res) {
+    if constexpr (MODE == 0) hipLaunchKernelGGL((conv_s8_kernel<TOC, TP, WOC, MODE, 0, true, true>), grid, block, 0, s, a);
+    else return hipErrorInvalidValue;
+  } else {
+    hipLaunchKernelGGL((conv_s8_kernel<TOC, TP, WOC, MODE, 0, false, true>), grid, block, 0, s, a);
   }
   return hipGetLastError();
 }
@@ -418,6 +477,12 @@ hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
   if (is_stem(a.C, a.kH, a.kW)) return launch_cfg<64, 256, 1, 1>(a, s);
   if (a.OCp == 64) return launch_cfg<64, 256, 1, 0>(a, s);
   return launch_cfg<128, 128, 2, 0>(a, s);
+}
+
+hipError_t launch_conv_f8(const ConvArgs& a, hipStream_t s) {
+  if (is_stem(a.C, a.kH, a.kW)) return launch_cfg_f8<64, 256, 1, 1>(a, s);
+  if (a.OCp == 64) return launch_cfg_f8<64, 256, 1, 0>(a, s);
+  return launch_cfg_f8<128, 128, 2, 0>(a, s);
 }
 
 hipError_t launch_quantize_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cout,

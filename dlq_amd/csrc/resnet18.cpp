@@ -99,6 +99,9 @@ struct dlq_resnet18 {
   // interleave and fill each other's tail waves
   hipStream_t s2 = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  // DLQ_PREC_INT8 / DLQ_PREC_FP8 (e4m3 activations + per-channel e4m3
+  // weights; generic packed layout in ConvLayer::w, fc_w row-major codes)
+  int prec = DLQ_PREC_INT8;
 };
 
 namespace {
@@ -349,6 +352,18 @@ void weights_s8(const dlq_resnet18* m, const std::string& name, int OC, int K, s
   quantize_weights(m->tensors.at(name).data(), OC, K, q.data(), sw.data());
 }
 
+// fp32 values of a weight tensor for the fp8 path: the fp32 tensor, or the
+// int8 manifest's q * scale[o] when only that was given.
+std::vector<float> weights_f32(const dlq_resnet18* m, const std::string& name, int OC, int K) {
+  auto t = m->tensors.find(name);
+  if (t != m->tensors.end()) return t->second;
+  const QTensor& qt = m->qtensors.at(name);
+  std::vector<float> w((size_t)OC * K);
+  for (int o = 0; o < OC; ++o)
+    for (int k = 0; k < K; ++k) w[(size_t)o * K + k] = (float)qt.q[(size_t)o * K + k] * qt.scale[o];
+  return w;
+}
+
 int check_ready(const dlq_resnet18* m) {
   for (const auto& n : required_tensors(m))
     if (!m->tensors.count(n) && !m->qtensors.count(n)) return fail(DLQ_ERR_STATE, "missing tensor: " + n);
@@ -574,12 +589,98 @@ int dlq_resnet18_load_scales(dlq_resnet18* m, const char* path) {
   return DLQ_OK;
 }
 
+}  // extern "C"
+
+namespace {
+template <typename T>
+int upload(dlq_resnet18* m, T** dst, const void* src, size_t bytes) {
+  int rc = dev_alloc(m, dst, bytes);
+  if (rc) return rc;
+  hipError_t e = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
+  return e == hipSuccess ? DLQ_OK : hip_fail(e, "weight upload");
+}
+
+// fp8 prepare: e4m3 per-channel weights in the generic packed layout, BN
+// folded exactly as the int8 path (fold_bn with the e4m3 weight scales),
+// FC row-major; workspace includes the unfused stem's buffers.
+int prepare_f8(dlq_resnet18* m, int max_batch) {
+  int rc;
+  for (auto& c : m->convs) {
+    const int K = c.IC * c.k * c.k, ocp = packed_oc(c.OC);
+    const std::vector<float> w = weights_f32(m, c.wname, c.OC, K);
+    std::vector<uint8_t> q((size_t)c.OC * K);
+    std::vector<float> sw(c.OC);
+    quantize_weights_f8(w.data(), c.OC, K, q.data(), sw.data());
+    std::vector<int8_t> packed(packed_bytes(c.OC, c.Cstore, c.k, c.k));
+    pack_conv_weights((const int8_t*)q.data(), c.OC, c.IC, c.k, c.k, c.Cstore, packed.data());
+    std::vector<float> alpha(ocp, 0.f), beta(ocp, 0.f);
+    fold_bn(m->scales.at(c.in_site), sw.data(), m->tensors.at(c.bn + ".weight").data(),
+            m->tensors.at(c.bn + ".bias").data(), m->tensors.at(c.bn + ".running_mean").data(),
+            m->tensors.at(c.bn + ".running_var").data(), 1e-5f, m->scales.at(c.site), c.OC, alpha.data(),
+            beta.data());
+    if ((rc = upload(m, &c.w, packed.data(), packed.size())) || (rc = upload(m, &c.alpha, alpha.data(), ocp * 4)) ||
+        (rc = upload(m, &c.beta, beta.data(), ocp * 4)))
+      return rc;
+  }
+  {
+    const int O = 1000, I = 512;
+    const std::vector<float> w = weights_f32(m, "fc.weight", O, I);
+    std::vector<uint8_t> q((size_t)O * I);
+    std::vector<float> sw(O), alpha(O), beta(O);
+    quantize_weights_f8(w.data(), O, I, q.data(), sw.data());
+    const float sg = m->scales.at("gap");
+    const std::vector<float>& bias = m->tensors.at("fc.bias");
+    for (int o = 0; o < O; ++o) {
+      alpha[o] = sg * sw[o];
+      beta[o] = bias[o];
+    }
+    if ((rc = upload(m, &m->fc_w, q.data(), q.size())) || (rc = upload(m, &m->fc_alpha, alpha.data(), O * 4)) ||
+        (rc = upload(m, &m->fc_beta, beta.data(), O * 4)))
+      return rc;
+  }
+  const size_t B = (size_t)max_batch;
+  if ((rc = dev_alloc(m, &m->gq, B * 512)) || (rc = dev_alloc(m, &m->xq, B * 224 * 224 * kStemC)) ||
+      (rc = dev_alloc(m, &m->c1, B * 112 * 112 * 64)))
+    return rc;
+  for (auto& b : m->buf)
+    if ((rc = dev_alloc(m, &b, B * 56 * 56 * 64))) return rc;
+  if (m->keep) {
+    const std::pair<const char*, size_t> kb[] = {{"stem_pool", 56 * 56 * 64}, {"layer1", 56 * 56 * 64},
+                                                 {"layer2", 28 * 28 * 128}, {"layer3", 14 * 14 * 256},
+                                                 {"layer4", 7 * 7 * 512}};
+    for (const auto& k : kb) {
+      int8_t* p = nullptr;
+      if ((rc = dev_alloc(m, &p, B * k.second))) return rc;
+      m->keepbuf[k.first] = p;
+    }
+  }
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail(e, "prepare sync");
+  m->max_batch = max_batch;
+  m->prepared = true;
+  return DLQ_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int dlq_resnet18_set_precision(dlq_resnet18* m, int precision) {
+  if (!m || (precision != DLQ_PREC_INT8 && precision != DLQ_PREC_FP8))
+    return fail(DLQ_ERR_ARG, "set_precision: DLQ_PREC_INT8 or DLQ_PREC_FP8");
+  if (m->prec != precision) {
+    m->prec = precision;
+    m->prepared = false;  // weights and workspace must be prepared again
+  }
+  return DLQ_OK;
+}
+
 int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
   if (!m || max_batch <= 0) return fail(DLQ_ERR_ARG, "prepare: bad args");
   int rc = check_ready(m);
   if (rc) return rc;
   free_all(m);
   hipStream_t s = (hipStream_t)stream;
+  if (m->prec == DLQ_PREC_FP8) return prepare_f8(m, max_batch);
   // Weights: quantise per output channel, fold BN, pack, upload once.
   for (auto& c : m->convs) {
     const int K = c.IC * c.k * c.k;
@@ -676,6 +777,7 @@ int dlq_basic_block_s8(dlq_resnet18* m, int block, const int8_t* x, int N, int8_
   if (N < 0 || N > m->max_batch) return fail(DLQ_ERR_ARG, "basic_block: batch exceeds prepared max_batch");
   if (N == 0) return DLQ_OK;
   if (!x || !y) return fail(DLQ_ERR_ARG, "basic_block: null pointer");
+  if (m->prec != DLQ_PREC_INT8) return fail(DLQ_ERR_STATE, "basic_block: int8 models only");
   const Block& b = m->blocks[block];
   const int H = m->convs[b.c1].H;
   int OH, OW;
@@ -688,8 +790,75 @@ namespace {
 // One forward pass over images [img0, img0 + B) of the workspace partition
 // starting at image img0 (every buffer is sized max_batch x the largest
 // per-image activation, so partitions of disjoint image ranges never overlap).
+// fp8 conv launch (generic implicit-GEMM kernel, e4m3 in and out).
+int conv_f8(dlq_resnet18* m, const ConvLayer& c, const int8_t* x, int N, int H, const int8_t* residual,
+            float s_res, bool relu, int8_t* y, hipStream_t s) {
+  int rc = mark(m, s, DLQ_FAM_F8);
+  if (rc) return rc;
+  dlq_conv_desc d{N, H, H, c.Cstore, c.OC, c.k, c.k, c.s, c.s, c.p, c.p};
+  const float r_s = residual ? dlq::res_scale(s_res, m->scales.at(c.site)) : 0.f;
+  return dlq_conv2d_nhwc_f8(&d, (const uint8_t*)x, (const uint8_t*)c.w, c.alpha, c.beta, (const uint8_t*)residual,
+                            r_s, relu ? 1 : 0, (uint8_t*)y, s);
+}
+
+// The fp8 forward (oracle.py resnet18_forward_f8): quantise -> conv1 ->
+// maxpool -> 8 blocks of 2-3 conv launches -> GAP -> FC.
+int forward_pass_f8(dlq_resnet18* m, const float* x, int B, float* logits, hipStream_t s, bool record) {
+  const size_t nB = (size_t)B;
+  int rc;
+  const ConvLayer& st = m->convs[m->stem];
+  if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
+  rc = dlq_quantize_nchw_to_nhwc_f8(x, B, 3, 224, 224, kStemC, inv_scale(m->scales.at("input")), (uint8_t*)m->xq, s);
+  if (rc) return rc;
+  if (record) m->stage["input_q"] = {m->xq, nB * 224 * 224 * kStemC};
+  if ((rc = conv_f8(m, st, m->xq, B, 224, nullptr, 0.f, true, m->c1, s))) return rc;
+  if (record) m->stage["conv1"] = {m->c1, nB * 112 * 112 * 64};
+  int ci = 0;
+  int8_t* cur = m->buf[ci];
+  if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
+  // post-ReLU e4m3 codes are 0x00..0x7e: their int8 max is the value max
+  if ((rc = dlq_maxpool2d_3x3_s2p1_nhwc_s8(m->c1, B, 64, 112, 112, cur, s))) return rc;
+  if (record && (rc = record_stage(m, "stem_pool", cur, nB * 56 * 56 * 64, s))) return rc;
+  int H = 56;
+  for (const Block& b : m->blocks) {
+    int fi[3], k = 0;
+    for (int i = 0; i < 4; ++i)
+      if (i != ci && k < 3) fi[k++] = i;
+    const ConvLayer& c1 = m->convs[b.c1];
+    const ConvLayer& c2 = m->convs[b.c2];
+    int8_t *h = m->buf[fi[0]], *dsb = m->buf[fi[1]], *out = m->buf[fi[2]];
+    if ((rc = conv_f8(m, c1, cur, B, H, nullptr, 0.f, true, h, s))) return rc;
+    const int8_t* skip = cur;
+    float s_skip = m->scales.at(c1.in_site);
+    if (b.down) {
+      const ConvLayer& ds = m->convs[b.ds];
+      if ((rc = conv_f8(m, ds, cur, B, H, nullptr, 0.f, false, dsb, s))) return rc;
+      skip = dsb;
+      s_skip = m->scales.at(ds.site);
+    }
+    const int OH = out_dim(H, 3, c1.s, 1);
+    if ((rc = conv_f8(m, c2, h, B, OH, skip, s_skip, true, out, s))) return rc;
+    ci = fi[2];
+    cur = out;
+    H = OH;
+    if (record && b.name.size() == 8 && b.name[7] == '1')
+      if ((rc = record_stage(m, b.name.substr(0, 6).c_str(), cur, nB * H * H * b.oc, s))) return rc;
+  }
+  const std::string last = m->convs[m->blocks.back().c2].site;
+  // gap_k * 2^-9 (oracle.py gap_k_f8): the sums are in e4m3 units of 2^-9
+  const float k = ((m->scales.at(last) / (float)(H * H)) / m->scales.at("gap")) * 0x1p-9f;
+  if ((rc = mark(m, s, DLQ_FAM_GAP))) return rc;
+  if ((rc = dlq_gap_nhwc_f8((const uint8_t*)cur, B, 512, H * H, k, (uint8_t*)m->gq, s))) return rc;
+  if (record) m->stage["gap"] = {m->gq, nB * 512};
+  if ((rc = mark(m, s, DLQ_FAM_FC))) return rc;
+  rc = dlq_linear_f8((const uint8_t*)m->gq, B, 512, (const uint8_t*)m->fc_w, 1000, m->fc_alpha, m->fc_beta, logits, s);
+  if (rc) return rc;
+  return mark(m, s, -1);
+}
+
 int forward_pass(dlq_resnet18* m, const float* x, int B, float* logits, hipStream_t s, size_t img0,
                  bool record) {
+  if (m->prec == DLQ_PREC_FP8) return forward_pass_f8(m, x, B, logits, s, record);
   const size_t nB = (size_t)B;
   constexpr size_t kAct = 56 * 56 * 64;  // largest per-image activation (buffer stride per image)
   void* stream = s;
@@ -761,7 +930,7 @@ bool use_split(const dlq_resnet18* m, int B) {
     const char* e = std::getenv("DLQ_SPLIT");
     return e && e[0] == '1';
   }();
-  return on && !m->timing && !m->keep && B >= 64;
+  return on && m->prec == DLQ_PREC_INT8 && !m->timing && !m->keep && B >= 64;
 }
 
 }  // namespace
@@ -834,6 +1003,21 @@ int dlq_resnet18_timing(dlq_resnet18* m, double* ms, int* launches, int* forward
 int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes) {
   if (!m || !macs || !bytes) return fail(DLQ_ERR_ARG, "family_work: null");
   for (int f = 0; f < DLQ_FAM_COUNT; ++f) macs[f] = bytes[f] = 0.0;
+  if (m->prec == DLQ_PREC_FP8) {  // every conv is one conv_s8_kernel<F8> launch
+    for (const ConvLayer& c : m->convs) {
+      const int OH = out_dim(c.H, c.k, c.s, c.p);
+      macs[DLQ_FAM_F8] += (double)c.OC * c.IC * c.k * c.k * OH * OH;
+      bytes[DLQ_FAM_F8] += (double)c.H * c.H * c.Cstore + (double)OH * OH * c.OC;
+    }
+    for (const Block& b : m->blocks) {  // conv2's residual read
+      const ConvLayer& c2 = m->convs[b.c2];
+      bytes[DLQ_FAM_F8] += (double)c2.H * c2.H * c2.OC;
+    }
+    macs[DLQ_FAM_FC] = 512.0 * 1000;
+    bytes[DLQ_FAM_FC] = 512.0 + 4000.0;
+    bytes[DLQ_FAM_GAP] = 7.0 * 7 * 512 + 512;
+    return DLQ_OK;
+  }
   // stem: fp32 input read + pooled int8 output written, 7x7x3 MACs at 112x112
   const ConvLayer& st = m->convs[m->stem];
   macs[DLQ_FAM_STEM] = (double)st.OC * st.IC * st.k * st.k * 112.0 * 112.0;

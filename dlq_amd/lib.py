@@ -19,9 +19,11 @@ LIB_PATH = os.path.join(_HERE, "libdlq.so")
 
 DLQ_OK = 0
 DLQ_OUT_S8, DLQ_OUT_F32, DLQ_OUT_S32 = 0, 1, 2
+DLQ_PREC_INT8, DLQ_PREC_FP8 = 0, 1
 # kernel families of dlq_resnet18_timing (include/dlq.h DLQ_FAM_*)
 FAMILIES = ["stem_fused_kernel", "block_l1_kernel (layer1 block)", "conv3x3s2i_kernel (+downsample)",
-            "conv3x3i_kernel (layer2-4 s1)", "gap16_kernel", "linear_kernel (fc)", "other"]
+            "conv3x3i_kernel (layer2-4 s1)", "gap16_kernel", "linear_kernel (fc)", "other",
+            "conv_s8_kernel fp8 (all convs, fp8 path)"]
 
 
 class DLQError(RuntimeError):
@@ -96,6 +98,16 @@ _SIGS = {
     "dlq_preprocess_u8": ([_vp, _i, _i, _i, _vp, _vp], _i),
     "dlq_softmax_f32": ([_vp, _i, _i, _vp, _vp], _i),
     "dlq_top1_f32": ([_vp, _i, _i, _vp, _vp, _vp], _i),
+    "dlq_quantize_weights_f8": ([_vp, _i, _i, _vp, _vp], _i),
+    "dlq_quantize_f32_f8": ([_vp, _sz, _f, _vp, _vp], _i),
+    "dlq_quantize_nchw_to_nhwc_f8": ([_vp, _i, _i, _i, _i, _i, _f, _vp, _vp], _i),
+    "dlq_conv_packed_bytes_f8": ([C.POINTER(ConvDesc)], _sz),
+    "dlq_pack_conv_weights_f8": ([C.POINTER(ConvDesc), _vp, _i, _vp], _i),
+    "dlq_conv2d_nhwc_f8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _f, _i, _vp, _vp], _i),
+    "dlq_conv2d_nhwc_f8_acc": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp], _i),
+    "dlq_gap_nhwc_f8": ([_vp, _i, _i, _i, _f, _vp, _vp], _i),
+    "dlq_linear_f8": ([_vp, _i, _i, _vp, _i, _vp, _vp, _vp, _vp], _i),
+    "dlq_resnet18_set_precision": ([_vp, _i], _i),
 }
 
 if not os.path.exists(LIB_PATH):

@@ -144,7 +144,7 @@ class ResNet18Int8:
     forward = 22 launches on the current stream, no host sync."""
 
     def __init__(self, sd: dict[str, np.ndarray], scales: dict[str, float], max_batch: int,
-                 keep_stages: bool = False):
+                 keep_stages: bool = False, precision: str = "int8"):
         from .lib import check, lib
         self._lib, self._check = lib, check
         h = C.c_void_p()
@@ -156,6 +156,10 @@ class ResNet18Int8:
         for site, s in scales.items():
             check(lib.dlq_resnet18_set_scale(h, site.encode(), float(s)), f"set_scale {site}")
         check(lib.dlq_resnet18_set_keep_stages(h, int(keep_stages)), "keep_stages")
+        if precision not in ("int8", "fp8"):
+            raise ValueError("precision must be 'int8' or 'fp8'")
+        self.precision = precision
+        check(lib.dlq_resnet18_set_precision(h, 1 if precision == "fp8" else 0), "set_precision")
         check(lib.dlq_resnet18_prepare(h, max_batch, None), "resnet18_prepare")
         self.max_batch = max_batch
 
@@ -187,16 +191,16 @@ class ResNet18Int8:
     def timing(self):
         """Per kernel family (lib.FAMILIES): (summed ms, launches), and the
         forwards covered since set_timing / the last call."""
-        ms = (C.c_double * 7)()
-        nl = (C.c_int * 7)()
+        ms = (C.c_double * 8)()
+        nl = (C.c_int * 8)()
         nf = C.c_int()
         self._check(self._lib.dlq_resnet18_timing(self.h, ms, nl, C.byref(nf)), "timing")
         return list(ms), list(nl), nf.value
 
     def family_work(self):
         """Per kernel family: (algorithmic MACs, activation bytes) per image and forward."""
-        macs = (C.c_double * 7)()
-        nbytes = (C.c_double * 7)()
+        macs = (C.c_double * 8)()
+        nbytes = (C.c_double * 8)()
         self._check(self._lib.dlq_resnet18_family_work(self.h, macs, nbytes), "family_work")
         return list(macs), list(nbytes)
 

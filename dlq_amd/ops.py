@@ -267,3 +267,91 @@ def top1(x: torch.Tensor):
     val = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
     check(lib.dlq_top1_f32(ptr(x), x.shape[0], x.shape[1], ptr(idx), ptr(val), stream_handle()), "top1")
     return idx, val
+
+
+# ------------------------------------------------------------ fp8 (e4m3) path
+# BASELINE configs[4]; include/dlq.h fp8 section.  e4m3 tensors are uint8
+# code tensors (torch.float8_e4m3fn bytes).
+
+def quantize_weights_f8(w: np.ndarray):
+    w = np.ascontiguousarray(w, np.float32)
+    OC = w.shape[0]
+    K = w.size // OC
+    q = np.empty(w.shape, np.uint8)
+    s = np.empty(OC, np.float32)
+    check(lib.dlq_quantize_weights_f8(w.ctypes.data, OC, K, q.ctypes.data, s.ctypes.data), "quantize_weights_f8")
+    return q, s
+
+
+def quantize_f32_f8(x: torch.Tensor, scale: float) -> torch.Tensor:
+    _dev(x, torch.float32)
+    y = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    inv = float(np.float32(1.0) / np.float32(scale))
+    check(lib.dlq_quantize_f32_f8(ptr(x), x.numel(), inv, ptr(y), stream_handle()), "quantize_f32_f8")
+    return y
+
+
+def quantize_nchw_to_nhwc_f8(x: torch.Tensor, scale: float, c_out: int = 4) -> torch.Tensor:
+    _dev(x, torch.float32)
+    N, Cc, H, W = x.shape
+    y = torch.empty((N, H, W, c_out), dtype=torch.uint8, device=x.device)
+    inv = float(np.float32(1.0) / np.float32(scale))
+    check(lib.dlq_quantize_nchw_to_nhwc_f8(ptr(x), N, Cc, H, W, c_out, inv, ptr(y), stream_handle()),
+          "quantize_nchw_to_nhwc_f8")
+    return y
+
+
+def pack_conv_weights_f8(q_oihw: np.ndarray, C_store: int) -> np.ndarray:
+    """Generic packed image of e4m3 OIHW codes (dlq_pack_conv_weights_f8)."""
+    q = np.ascontiguousarray(q_oihw, np.uint8)
+    OC, IC, k, _ = q.shape
+    d = ConvDesc(1, 1, 1, C_store, OC, k, k, 1, 1, 0, 0)
+    nb = lib.dlq_conv_packed_bytes_f8(C.byref(d))
+    if nb == 0:
+        raise ValueError("unsupported conv shape for the fp8 path")
+    out = np.empty(nb, np.uint8)
+    check(lib.dlq_pack_conv_weights_f8(C.byref(d), q.ctypes.data, IC, out.ctypes.data), "pack_conv_weights_f8")
+    return out
+
+
+def conv2d_nhwc_f8(x: torch.Tensor, w_packed: torch.Tensor, OC: int, k: int, stride: int, pad: int,
+                   alpha: torch.Tensor, beta: torch.Tensor, residual: torch.Tensor | None = None,
+                   res_scale: float = 0.0, relu: bool = True) -> torch.Tensor:
+    _dev(x, torch.uint8)
+    N, H, W, Cc = x.shape
+    OH, OW = out_dim(H, k, stride, pad), out_dim(W, k, stride, pad)
+    y = torch.empty((N, OH, OW, OC), dtype=torch.uint8, device=x.device)
+    d = ConvDesc(N, H, W, Cc, OC, k, k, stride, stride, pad, pad)
+    check(lib.dlq_conv2d_nhwc_f8(C.byref(d), ptr(x), ptr(w_packed), ptr(alpha), ptr(beta), ptr(residual),
+                                 float(res_scale), int(relu), ptr(y), stream_handle()), "conv2d_nhwc_f8")
+    return y
+
+
+def conv2d_nhwc_f8_acc(x: torch.Tensor, w_packed: torch.Tensor, OC: int, k: int, stride: int, pad: int):
+    """Raw fp32 accumulators [N,OH,OW,OC] of the e4m3 conv (parity/debugging)."""
+    _dev(x, torch.uint8)
+    N, H, W, Cc = x.shape
+    OH, OW = out_dim(H, k, stride, pad), out_dim(W, k, stride, pad)
+    y = torch.empty((N, OH, OW, OC), dtype=torch.float32, device=x.device)
+    d = ConvDesc(N, H, W, Cc, OC, k, k, stride, stride, pad, pad)
+    check(lib.dlq_conv2d_nhwc_f8_acc(C.byref(d), ptr(x), ptr(w_packed), ptr(y), stream_handle()),
+          "conv2d_nhwc_f8_acc")
+    return y
+
+
+def gap_nhwc_f8(x: torch.Tensor, k: float) -> torch.Tensor:
+    _dev(x, torch.uint8)
+    N, H, W, Cc = x.shape
+    y = torch.empty((N, Cc), dtype=torch.uint8, device=x.device)
+    check(lib.dlq_gap_nhwc_f8(ptr(x), N, Cc, H * W, float(k), ptr(y), stream_handle()), "gap_nhwc_f8")
+    return y
+
+
+def linear_f8(x: torch.Tensor, w: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor) -> torch.Tensor:
+    _dev(x, torch.uint8)
+    _dev(w, torch.uint8)
+    N, K = x.shape
+    O = w.shape[0]
+    y = torch.empty((N, O), dtype=torch.float32, device=x.device)
+    check(lib.dlq_linear_f8(ptr(x), N, K, ptr(w), O, ptr(alpha), ptr(beta), ptr(y), stream_handle()), "linear_f8")
+    return y

@@ -17,7 +17,9 @@ from .models import BLOCKS, torch_resnet18
 
 
 @torch.inference_mode()
-def calibrate_resnet18(sd, x: torch.Tensor, device=None) -> dict[str, float]:
+def calibrate_resnet18(sd, x: torch.Tensor, device=None, qmax: float = 127.0) -> dict[str, float]:
+    """Per-site scales amax / qmax: qmax 127 for int8, 448 (the e4m3 maximum)
+    for the fp8 path."""
     device = device or x.device
     m = torch_resnet18(sd, device)
     x = x.to(device)
@@ -46,7 +48,7 @@ def calibrate_resnet18(sd, x: torch.Tensor, device=None) -> dict[str, float]:
         upd(f"{name}.conv2", y)
     g = F.adaptive_avg_pool2d(y, 1).flatten(1)
     upd("gap", g)
-    return {k: float(np.float32(max(v, 1e-8) / 127.0)) for k, v in amax.items()}
+    return {k: float(np.float32(max(v, 1e-8) / qmax)) for k, v in amax.items()}
 
 
 def save_scales(scales: dict[str, float], path: str) -> None:

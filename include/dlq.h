@@ -320,7 +320,8 @@ enum {
   DLQ_FAM_GAP = 4,   /* gap16_kernel                                            */
   DLQ_FAM_FC = 5,    /* linear_kernel (FC)                                      */
   DLQ_FAM_OTHER = 6, /* any unfused fallback launch                             */
-  DLQ_FAM_COUNT = 7
+  DLQ_FAM_F8 = 7,    /* conv_s8_kernel<..., F8>: every conv of the fp8 path     */
+  DLQ_FAM_COUNT = 8
 };
 int dlq_resnet18_set_timing(dlq_resnet18* m, int on);
 int dlq_resnet18_timing(dlq_resnet18* m, double* ms, int* launches, int* forwards);
@@ -365,6 +366,50 @@ int dlq_softmax_f32(const float* x, int N, int K, float* y, void* stream);
  * the first index whose logit beats the running best (initially -1e30);
  * idx = -1 if none does.  val may be NULL. */
 int dlq_top1_f32(const float* x, int N, int K, int* idx, float* val, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* fp8 (e4m3) variant: BASELINE configs[4] / SURVEY.md §8(f) row 4.  No     */
+/* reference code exists for it (the reference is fp32 + this build's int8 */
+/* scheme); each entry point below is the e4m3 twin of the int8 one named.  */
+/* Values are OCP e4m3fn bytes (uint8): activations at a per-tensor scale   */
+/* (amax/448), weights per output channel (max|w|/448).  Requantisation:    */
+/* clamp(y, lo, 448), -0 -> +0, round to nearest even (lo = 0 with ReLU,    */
+/* -448 without).  Conv products accumulate in fp32 on                      */
+/* v_mfma_f32_32x32x64_f8f6f4; GAP and FC are exact (see oracle.c).         */
+/* ------------------------------------------------------------------------ */
+/* twin of dlq_quantize_weights_s8: scale[o] = max|w|/448 (1 if zero). */
+int dlq_quantize_weights_f8(const float* w, int OC, int K, uint8_t* q, float* scale);
+/* twin of dlq_quantize_f32_s8 (x 16-B aligned, q 4-B aligned). */
+int dlq_quantize_f32_f8(const float* x, size_t n, float inv_s, uint8_t* q, void* stream);
+/* twin of dlq_quantize_nchw_to_nhwc_s8. */
+int dlq_quantize_nchw_to_nhwc_f8(const float* x, int N, int C, int H, int W, int Cout, float inv_s, uint8_t* y,
+                                 void* stream);
+/* Generic packed image (C % 64 == 0 or the 7x7 C == 4 stem; the wide int8
+ * layouts are not used by the fp8 path). */
+size_t dlq_conv_packed_bytes_f8(const dlq_conv_desc* d);
+int dlq_pack_conv_weights_f8(const dlq_conv_desc* d, const uint8_t* q_oihw, int IC, uint8_t* packed);
+/* twin of dlq_conv2d_nhwc_s8 (DLQ_OUT_S8 semantics, e4m3 in and out):
+ *   y = fmaf(acc, alpha[o], beta[o]) [+ fmaf(dec(res), res_scale, y)], requant. */
+int dlq_conv2d_nhwc_f8(const dlq_conv_desc* d, const uint8_t* x, const uint8_t* w_packed, const float* alpha,
+                       const float* beta, const uint8_t* residual, float res_scale, int relu, uint8_t* y,
+                       void* stream);
+/* The raw fp32 accumulators of the same conv (twin of DLQ_OUT_S32): acc
+ * NHWC [N][OH][OW][OC] fp32 (parity / debugging). */
+int dlq_conv2d_nhwc_f8_acc(const dlq_conv_desc* d, const uint8_t* x, const uint8_t* w_packed, float* acc,
+                           void* stream);
+/* twin of dlq_gap_nhwc_s8: exact sum of the values in units of 2^-9, then
+ * requant(float(sum) * k) with k = s_in/HW/s_out * 2^-9.  The int8
+ * dlq_maxpool2d_3x3_s2p1_nhwc_s8 applies unchanged to non-negative e4m3. */
+int dlq_gap_nhwc_f8(const uint8_t* x, int N, int C, int HW, float k, uint8_t* y, void* stream);
+/* twin of dlq_fc_s8: logits[N][O] = fmaf(float(acc), alpha[o], beta[o]), acc
+ * exact (fp64); w row-major [O][K] e4m3 (not packed). */
+int dlq_linear_f8(const uint8_t* x, int N, int K, const uint8_t* w, int O, const float* alpha, const float* beta,
+                  float* y, void* stream);
+/* Engine precision (before dlq_resnet18_prepare): DLQ_PREC_INT8 (default)
+ * or DLQ_PREC_FP8 (activation scales then calibrated as amax/448). */
+#define DLQ_PREC_INT8 0
+#define DLQ_PREC_FP8 1
+int dlq_resnet18_set_precision(dlq_resnet18* m, int precision);
 
 #ifdef __cplusplus
 }

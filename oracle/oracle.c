@@ -378,3 +378,170 @@ ORA_API void ora_mlp_layer_s8_acc(const int8_t* x, const int8_t* Wt, int B, int 
     }
   }
 }
+
+/* ------------------------------------------------------------------ */
+/* fp8 path (BASELINE configs[4]; build-defined, */
+/* DESIGN.md §3b).  No reference code exists for it.                    */
+/* ------------------------------------------------------------------ */
+/* Values are OCP e4m3fn bytes: sign, 4 exponent bits (bias 7), 3 mantissa
+ * bits, max 448, 0x7F/0xFF NaN (never produced: every encode clamps to
+ * +-448 first).  Every e4m3 value is an integer multiple of 2^-9 (the
+ * smallest subnormal), so a code's "units" (value * 512) are an exact
+ * integer <= 229376, products of units are exact int64 multiples of 2^-18
+ * and every sum here is exact: the oracle's conv / FC accumulators are the
+ * exact real sums, returned as doubles (exact: |sum| * 2^18 < 2^53). */
+
+static int32_t f8_units_tab[256];
+static int f8_tab_ready = 0;
+
+static void f8_init(void) {
+  if (f8_tab_ready) return;
+  for (int c = 0; c < 256; ++c) {
+    const int e = (c >> 3) & 15, m = c & 7;
+    /* subnormal: m * 2^-9 -> m units; normal: (8+m) * 2^(e-7-3) -> (8+m) << (e-1) units */
+    int32_t u = e == 0 ? m : (8 + m) << (e - 1);
+    if ((c & 0x7f) == 0x7f) u = 0; /* NaN: never produced or consumed */
+    f8_units_tab[c] = (c & 0x80) ? -u : u;
+  }
+  f8_tab_ready = 1;
+}
+
+ORA_API float ora_f8_decode(uint8_t c) {
+  f8_init();
+  float v = ldexpf((float)f8_units_tab[c], -9);
+  if (c == 0x80) v = -0.0f;
+  return v;
+}
+
+/* Round-to-nearest-even e4m3 encode of y, |y| <= 448 (callers clamp).  The
+ * sign bit is y's (a negative value that rounds to zero gives 0x80). */
+static uint8_t f8_encode(float y) {
+  const uint8_t sgn = signbit(y) ? 0x80 : 0;
+  const float a = fabsf(y);
+  uint8_t code;
+  if (a < 0x1p-6f) {
+    code = (uint8_t)(int)rintf(a * 512.f); /* subnormal grid 2^-9; 8 = smallest normal */
+  } else {
+    int e;
+    frexpf(a, &e);                /* a = f * 2^e, f in [0.5, 1) -> unbiased exponent e-1 */
+    const int E = e - 1;          /* -6 .. 8 */
+    int r = (int)rintf(ldexpf(a, 3 - E)); /* mantissa with hidden bit, 8 .. 16 */
+    int eb = E + 7;
+    if (r == 16) { r = 8; ++eb; }
+    code = (uint8_t)((eb << 3) | (r - 8));
+  }
+  return code | sgn;
+}
+
+/* clamp(y, lo, 448), -0 -> +0 (y + 0.0f), encode: the requantisation of the
+ * fp8 scheme, repeated op for op by device_common.h enc4_f8. */
+static inline uint8_t f8_requant(float y, float lo) {
+  y = y < lo ? lo : y;
+  y = y > 448.f ? 448.f : y;
+  return f8_encode(y + 0.0f);
+}
+
+ORA_API void ora_encode_f8(const float* y, size_t n, uint8_t* q) {
+  for (size_t i = 0; i < n; ++i) q[i] = f8_encode(y[i]);
+}
+
+ORA_API void ora_decode_f8(const uint8_t* q, size_t n, float* y) {
+  for (size_t i = 0; i < n; ++i) y[i] = ora_f8_decode(q[i]);
+}
+
+/* fp32 -> e4m3 activation quantisation: q = requant(x * inv_s, -448). */
+ORA_API void ora_quantize_f32_f8(const float* x, size_t n, float inv_s, uint8_t* q) {
+  for (size_t i = 0; i < n; ++i) q[i] = f8_requant(x[i] * inv_s, -448.f);
+}
+
+/* Per-output-channel e4m3 weights: s[o] = max|w|/448 (1 if all zero),
+ * q = requant(w / s, -448). */
+ORA_API void ora_quantize_weights_f8(const float* w, int OC, int K, uint8_t* q, float* scale) {
+  for (int o = 0; o < OC; ++o) {
+    float mx = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float a = fabsf(w[(size_t)o * K + k]);
+      mx = a > mx ? a : mx;
+    }
+    const float s = mx > 0.f ? mx / 448.f : 1.f;
+    scale[o] = s;
+    for (int k = 0; k < K; ++k) q[(size_t)o * K + k] = f8_requant(w[(size_t)o * K + k] / s, -448.f);
+  }
+}
+
+/* Exact accumulators of an e4m3 conv (NCHW codes, OIHW codes), as doubles. */
+ORA_API int ora_conv2d_nchw_f8_acc(const uint8_t* x, int N, int IC, int H, int W, const uint8_t* w, int OC,
+                                   int kH, int kW, int sH, int sW, int pH, int pW, double* acc) {
+  f8_init();
+  const int OH = out_dim(H, kH, sH, pH), OW = out_dim(W, kW, sW, pW);
+  const size_t K = (size_t)IC * kH * kW, P = (size_t)OH * OW;
+  int8_t* col = (int8_t*)malloc(K * P);
+  int32_t* cu = (int32_t*)malloc(K * P * sizeof(int32_t));
+  int64_t* row = (int64_t*)malloc(P * sizeof(int64_t));
+  if (!col || !cu || !row) {
+    free(col); free(cu); free(row);
+    return 1;
+  }
+  for (int n = 0; n < N; ++n) {
+    /* zero padding = code 0x00 = +0 */
+    ora_im2col_nchw_s8((const int8_t*)x + (size_t)n * IC * H * W, IC, H, W, kH, kW, sH, sW, pH, pW, col);
+    for (size_t i = 0; i < K * P; ++i) cu[i] = f8_units_tab[(uint8_t)col[i]];
+    for (int o = 0; o < OC; ++o) {
+      memset(row, 0, P * sizeof(int64_t));
+      for (size_t k = 0; k < K; ++k) {
+        const int64_t a = f8_units_tab[w[(size_t)o * K + k]];
+        if (!a) continue;
+        const int32_t* c = cu + k * P;
+        for (size_t p = 0; p < P; ++p) row[p] += a * c[p];
+      }
+      double* d = acc + ((size_t)n * OC + o) * P;
+      for (size_t p = 0; p < P; ++p) d[p] = ldexp((double)row[p], -18);
+    }
+  }
+  free(col); free(cu); free(row);
+  return 0;
+}
+
+/* fp8 fused epilogue on NCHW accumulators (alpha/beta/r_s in output-grid
+ * units, as ora_epilogue_s8):
+ *   y = fmaf(float(acc), alpha[c], beta[c]);  y = fmaf(dec(res), r_s, y)
+ *   q = requant(y, relu ? 0 : -448)                                       */
+ORA_API void ora_epilogue_f8(const double* acc, int N, int OC, int HW, const float* alpha, const float* beta,
+                             const uint8_t* res, float r_s, int relu, uint8_t* out) {
+  const float lo = relu ? 0.f : -448.f;
+  for (int n = 0; n < N; ++n)
+    for (int c = 0; c < OC; ++c)
+      for (int i = 0; i < HW; ++i) {
+        const size_t idx = ((size_t)n * OC + c) * HW + i;
+        float y = fmaf((float)acc[idx], alpha[c], beta[c]);
+        if (res) y = fmaf(ora_f8_decode(res[idx]), r_s, y);
+        out[idx] = f8_requant(y, lo);
+      }
+}
+
+/* GAP on e4m3: exact unit sums S (int32), y = requant(float(S) * k, -448)
+ * with k = gap_k(s_in, hw, s_out) * 2^-9 (the units' scale). */
+ORA_API void ora_gap_f8(const uint8_t* x, int N, int C, int HW, float k, int32_t* sums, uint8_t* y) {
+  f8_init();
+  for (int nc = 0; nc < N * C; ++nc) {
+    int32_t s = 0;
+    for (int i = 0; i < HW; ++i) s += f8_units_tab[x[(size_t)nc * HW + i]];
+    if (sums) sums[nc] = s;
+    y[nc] = f8_requant((float)s * k, -448.f);
+  }
+}
+
+/* FC on e4m3: exact acc, logits = fmaf(float(acc), alpha[o], beta[o]). */
+ORA_API void ora_fc_f8(const uint8_t* x, int N, int I, const uint8_t* W, int O, const float* alpha,
+                       const float* beta, double* accs, float* out) {
+  f8_init();
+  for (int n = 0; n < N; ++n)
+    for (int o = 0; o < O; ++o) {
+      int64_t s = 0;
+      for (int k = 0; k < I; ++k)
+        s += (int64_t)f8_units_tab[x[(size_t)n * I + k]] * f8_units_tab[W[(size_t)o * I + k]];
+      const double a = ldexp((double)s, -18);
+      if (accs) accs[(size_t)n * O + o] = a;
+      out[(size_t)n * O + o] = fmaf((float)a, alpha[o], beta[o]);
+    }
+}

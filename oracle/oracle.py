@@ -23,6 +23,8 @@ _LIB = None
 _f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
 _s8p = np.ctypeslib.ndpointer(np.int8, flags="C_CONTIGUOUS")
 _s32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
 _i = C.c_int
 _f = C.c_float
 
@@ -51,6 +53,14 @@ _SIGS = {
     "ora_gap_s8": [_s8p, _i, _i, _i, _f, C.c_void_p, _s8p],
     "ora_fc_s8": [_s8p, _i, _i, _s8p, _i, _f32p, _f32p, C.c_void_p, _f32p],
     "ora_mlp_layer_s8_acc": [_s8p, _s8p, _i, _i, _i, _s32p],
+    "ora_encode_f8": [_f32p, C.c_size_t, _u8p],
+    "ora_decode_f8": [_u8p, C.c_size_t, _f32p],
+    "ora_quantize_f32_f8": [_f32p, C.c_size_t, _f, _u8p],
+    "ora_quantize_weights_f8": [_f32p, _i, _i, _u8p, _f32p],
+    "ora_conv2d_nchw_f8_acc": [_u8p, _i, _i, _i, _i, _u8p, _i, _i, _i, _i, _i, _i, _i, _f64p],
+    "ora_epilogue_f8": [_f64p, _i, _i, _i, _f32p, _f32p, C.c_void_p, _f, _i, _u8p],
+    "ora_gap_f8": [_u8p, _i, _i, _i, _f, C.c_void_p, _u8p],
+    "ora_fc_f8": [_u8p, _i, _i, _u8p, _i, _f32p, _f32p, C.c_void_p, _f32p],
 }
 
 
@@ -64,7 +74,8 @@ def lib():
         for name, args in _SIGS.items():
             fn = getattr(L, name)
             fn.argtypes = args
-            fn.restype = {"ora_conv2d_nchw_s8_acc": C.c_int, "ora_res_scale": C.c_float}.get(name)
+            fn.restype = {"ora_conv2d_nchw_s8_acc": C.c_int, "ora_conv2d_nchw_f8_acc": C.c_int,
+                         "ora_res_scale": C.c_float}.get(name)
         _LIB = L
     return _LIB
 
@@ -327,6 +338,137 @@ def resnet18_forward_s8(sd, scales, x, eps=1e-5):
     dumps["gap"] = g
     wq, sw = quantize_weights_s8(sd["fc.weight"])
     logits, accs = fc_s8(g, wq, fc_alpha(scales["gap"], sw), sd["fc.bias"])
+    dumps["fc.acc"] = accs
+    dumps["logits"] = logits
+    return logits, dumps
+
+
+# ------------------------------------------------------------------ fp8 path
+# Config 5 (BASELINE configs[4]): e4m3 activations and
+# per-output-channel e4m3 weights.  No reference code exists; the scheme is
+# the build's own and oracle.c's ora_*_f8 functions define
+# it.  The e4m3 codec is pinned against torch.float8_e4m3fn
+# (tests/test_oracle_f8.py); accumulators here are EXACT (see oracle.c), so
+# the GPU's fp32 MFMA accumulation is checked with a stated tolerance.
+
+F8_MAX = 448.0
+
+
+def encode_f8(y):
+    """RNE e4m3fn codes (uint8) of fp32 values with |y| <= 448."""
+    y = _c(y, np.float32)
+    q = np.empty(y.shape, np.uint8)
+    lib().ora_encode_f8(y, y.size, q)
+    return q
+
+
+def decode_f8(q):
+    q = _c(q, np.uint8)
+    y = np.empty(q.shape, np.float32)
+    lib().ora_decode_f8(q, q.size, y)
+    return y
+
+
+def quantize_f32_f8(x, s):
+    x = _c(x, np.float32)
+    q = np.empty(x.shape, np.uint8)
+    lib().ora_quantize_f32_f8(x, x.size, inv_scale(s), q)
+    return q
+
+
+def quantize_weights_f8(w):
+    w = _c(w, np.float32)
+    OC = w.shape[0]; K = w.size // OC
+    q = np.empty(w.shape, np.uint8); s = np.empty(OC, np.float32)
+    lib().ora_quantize_weights_f8(w, OC, K, q, s)
+    return q, s
+
+
+def conv_f8_acc(x, wq, stride, pad):
+    """Exact accumulators (float64) of an e4m3 conv, NCHW codes x, OIHW codes wq."""
+    x = _c(x, np.uint8); wq = _c(wq, np.uint8)
+    N, IC, H, W = x.shape; OC, _, kH, kW = wq.shape
+    OH, OW = out_dim(H, kH, stride, pad), out_dim(W, kW, stride, pad)
+    acc = np.empty((N, OC, OH, OW), np.float64)
+    rc = lib().ora_conv2d_nchw_f8_acc(x, N, IC, H, W, wq, OC, kH, kW, stride, stride, pad, pad, acc)
+    assert rc == 0
+    return acc
+
+
+def epilogue_f8(acc, alpha, beta, res=None, r_s=0.0, relu=True):
+    N, OC = acc.shape[:2]; HW = int(np.prod(acc.shape[2:]))
+    out = np.empty(acc.shape, np.uint8)
+    r = None if res is None else _c(res, np.uint8)
+    lib().ora_epilogue_f8(_c(acc, np.float64), N, OC, HW, _c(alpha, np.float32), _c(beta, np.float32),
+                          _ptr(r), np.float32(r_s), int(relu), out)
+    return out
+
+
+def gap_k_f8(s_in, hw, s_out):
+    """GAP constant on e4m3 units: gap_k(...) * 2^-9 (exact)."""
+    return np.float32(gap_k(s_in, hw, s_out) * np.float32(2.0 ** -9))
+
+
+def gap_f8(x, k):
+    x = _c(x, np.uint8)
+    N, Cc = x.shape[:2]; HW = int(np.prod(x.shape[2:]))
+    sums = np.empty((N, Cc), np.int32); y = np.empty((N, Cc), np.uint8)
+    lib().ora_gap_f8(x, N, Cc, HW, np.float32(k), _ptr(sums), y)
+    return y, sums
+
+
+def fc_f8(x, wq, alpha, beta):
+    x = _c(x, np.uint8); wq = _c(wq, np.uint8)
+    N, I = x.shape; O = wq.shape[0]
+    accs = np.empty((N, O), np.float64); out = np.empty((N, O), np.float32)
+    lib().ora_fc_f8(x, N, I, wq, O, _c(alpha, np.float32), _c(beta, np.float32), _ptr(accs), out)
+    return out, accs
+
+
+def resnet18_forward_f8(sd, scales, x, eps=1e-5):
+    """fp8 (e4m3) forward of x[N,3,224,224] fp32 under activation scales
+    calibrated for the e4m3 range (amax / 448).  Same wiring and dump names
+    as resnet18_forward_s8; stage dumps are e4m3 codes (uint8), '.acc'
+    dumps exact float64 accumulators."""
+    dumps = {}
+    xq = quantize_f32_f8(x, scales["input"])
+    dumps["input_q"] = xq
+
+    def conv(name, xin, s_in, w, bn, stride, pad, res=None, s_res=0.0, relu=True):
+        wq, sw = quantize_weights_f8(w)
+        alpha, beta = fold_bn(s_in, sw, bn, scales[name], eps)
+        acc = conv_f8_acc(xin, wq, stride, pad)
+        dumps[name + ".acc"] = acc
+        r_s = res_scale(s_res, scales[name]) if res is not None else 0.0
+        out = epilogue_f8(acc, alpha, beta, res, r_s, relu=relu)
+        dumps[name] = out
+        return out
+
+    y = conv("conv1", xq, scales["input"], sd["conv1.weight"], _bn(sd, "bn1"), 2, 3)
+    # max over non-negative e4m3 codes (post-ReLU, -0 canonicalised) = max of
+    # the int8 bytes: the int8 maxpool applies unchanged
+    y = maxpool_s8(y.view(np.int8)).view(np.uint8)
+    dumps["stem_pool"] = y
+    s_y = scales["conv1"]
+    for name, ic, oc, s, ds in BLOCKS:
+        h = conv(f"{name}.conv1", y, s_y, sd[f"{name}.conv1.weight"], _bn(sd, f"{name}.bn1"), s, 1)
+        if ds:
+            skip = conv(f"{name}.downsample", y, s_y, sd[f"{name}.downsample.0.weight"],
+                        _bn(sd, f"{name}.downsample.1"), s, 0, relu=False)
+            s_skip = scales[f"{name}.downsample"]
+        else:
+            skip, s_skip = y, s_y
+        y = conv(f"{name}.conv2", h, scales[f"{name}.conv1"], sd[f"{name}.conv2.weight"],
+                 _bn(sd, f"{name}.bn2"), 1, 1, res=skip, s_res=s_skip)
+        s_y = scales[f"{name}.conv2"]
+        if name in STAGE_END:
+            dumps[STAGE_END[name]] = y
+    k = gap_k_f8(s_y, y.shape[2] * y.shape[3], scales["gap"])
+    g, sums = gap_f8(y, k)
+    dumps["gap_sum"] = sums
+    dumps["gap"] = g
+    wq, sw = quantize_weights_f8(sd["fc.weight"])
+    logits, accs = fc_f8(g, wq, fc_alpha(scales["gap"], sw), sd["fc.bias"])
     dumps["fc.acc"] = accs
     dumps["logits"] = logits
     return logits, dumps

@@ -48,6 +48,40 @@ def model_and_scales(seed=0x20260306, n_calib=2):
     return sd, scales
 
 
+@functools.lru_cache(maxsize=None)
+def model_and_scales_f8(seed=0x20260306, n_calib=2):
+    """Same weights, activation scales for the e4m3 range (amax / 448)."""
+    import torch
+    from dlq_amd.models import resnet18_state_dict, synthetic_images
+    from dlq_amd.quant import calibrate_resnet18
+    sd = resnet18_state_dict(seed)
+    torch.manual_seed(0)
+    scales = calibrate_resnet18(sd, synthetic_images(n_calib, seed=seed + 1), device="cpu", qmax=448.0)
+    return sd, scales
+
+
+def f8_ordinal(q):
+    """e4m3 codes -> signed ordinal (adjacent values differ by 1; +-0 -> 0)."""
+    q = np.asarray(q, np.uint8).astype(np.int32)
+    return np.where(q & 0x80, -(q & 0x7F), q)
+
+
+def f8_sweep(rng, n=60000):
+    """fp32 values covering the e4m3 range: random magnitudes over 2^-12..2^9
+    (beyond +-448 too), every exact e4m3 value, every rounding midpoint and
+    its two fp32 neighbours, both signs."""
+    from oracle import oracle as O
+    vals = O.decode_f8(np.arange(256, dtype=np.uint8))
+    vals = vals[np.isfinite(vals)]
+    pos = np.unique(np.abs(vals)).astype(np.float64)
+    mids = ((pos[1:] + pos[:-1]) / 2).astype(np.float32)
+    near = np.concatenate([mids, np.nextafter(mids, np.float32(0)), np.nextafter(mids, np.float32(1e9))])
+    mag = (2.0 ** rng.uniform(-12, 9.5, n)).astype(np.float32)
+    sgn = np.where(rng.random(n) < 0.5, -1, 1).astype(np.float32)
+    x = np.concatenate([mag * sgn, vals, near, -near, np.float32([0.0, -0.0, 448.0, -448.0, 1e6, -1e6])])
+    return x.astype(np.float32)
+
+
 def synth_image(h, w, seed):
     """Seeded smooth + noisy u8 HWC RGB image (tools/make_preprocess_golden.py
     generated the preprocessing goldens from exactly these)."""

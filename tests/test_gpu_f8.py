@@ -1,0 +1,186 @@
+"""GPU parity of the fp8 (e4m3) path through the C ABI vs the CPU oracle
+(oracle.c ora_*_f8).
+
+Bar, stated per kernel:
+  * quantisation (fp32 -> e4m3), GAP, FC: bit-exact (the same IEEE ops; GAP
+    sums exact integer units; FC accumulates exact products in fp64).
+  * convs: the oracle's accumulator is the exact sum; the MFMA's is not
+    IEEE fp32: tools/f8_acc_probe.py measured v_mfma_f32_32x32x64_f8f6f4
+    accumulators within 2^-18 * sum|w x| of the exact sum (errors unbiased,
+    ~10x fp32 rounding; internal dot precision, not the K-step adds).  With
+    E = 2^-16 * |alpha| * sum|w x| (4x that, sum|w x| exact from the
+    oracle), every output must satisfy
+        |dec(gpu) - dec(oracle)| <= step(e4m3 at that magnitude) + 2 E
+    i.e. at most one rounding flip away from the exact result, and at most
+    0.1 % of the outputs may differ at all.
+  * the whole network: a one-step flip of an input code moves each output
+    it feeds by ~1/sqrt(taps) of its own value, a sizeable fraction of the
+    coarse e4m3 step (12.5 %), so flips cascade through the 20 convs and
+    code-level equality is not a meaningful bar past the first layer.  The
+    first stage (stem_pool) keeps a code-level bound (<= 1 % differ); later
+    stages are compared decoded (cosine >= 0.99 against the oracle's fp8
+    forward) and the logits must track the fp32 reference as closely as the
+    oracle's own fp8 logits do (cosine >= 0.995, test_oracle_f8.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests.helpers import f8_sweep, model_and_scales_f8, nchw_to_nhwc, nhwc_to_nchw, rand_conv
+
+pytestmark = pytest.mark.gpu
+
+CONV_SHAPES = [
+    ("stem", 3, 64, 7, 2, 3, 224),
+    ("l1_3x3", 64, 64, 3, 1, 1, 56),
+    ("l2_0_conv1", 64, 128, 3, 2, 1, 56),
+    ("l2_3x3", 128, 128, 3, 1, 1, 28),
+    ("l2_ds", 64, 128, 1, 2, 0, 56),
+    ("l3_3x3", 256, 256, 3, 1, 1, 14),
+    ("l4_0_conv1", 256, 512, 3, 2, 1, 14),
+    ("l4_3x3", 512, 512, 3, 1, 1, 7),
+    ("l4_ds", 256, 512, 1, 2, 0, 14),
+]
+
+
+def _cuda(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _step(v):
+    """e4m3 spacing at magnitude v (2^-9 in the subnormal range)."""
+    v = np.maximum(np.abs(v), 2.0 ** -6)
+    return 2.0 ** (np.floor(np.log2(v)) - 3)
+
+
+def _check_conv(got, ref, err_bound, frac, what):
+    a, b = O.decode_f8(got).astype(np.float64), O.decode_f8(ref).astype(np.float64)
+    lim = _step(np.maximum(np.abs(a), np.abs(b))) + 2 * err_bound
+    bad = np.abs(a - b) > lim
+    n = np.count_nonzero(got != ref)
+    assert not bad.any(), (f"{what}: {np.count_nonzero(bad)} outputs beyond one step + 2E, e.g. "
+                           f"gpu={a[bad][:4]} ora={b[bad][:4]} E={err_bound[bad][:4]}")
+    assert n <= frac * got.size, f"{what}: {n} of {got.size} outputs differ (> {frac:%})"
+    return n
+
+
+def _close_codes(got, ref, frac, what):
+    n = np.count_nonzero(got != ref)
+    assert n <= frac * got.size, f"{what}: {n} of {got.size} codes differ (> {frac:%})"
+    return n
+
+
+def test_quantize_f32_f8_bitexact(gpu):
+    from dlq_amd import ops
+    rng = np.random.default_rng(11)
+    x = f8_sweep(rng)
+    x = np.concatenate([x, np.zeros((-len(x)) % 4 + 3, np.float32)])  # ragged tail (n % 4 == 3)
+    for s in (1.0, 0.37):
+        got = ops.quantize_f32_f8(_cuda(x), s).cpu().numpy()
+        ref = O.quantize_f32_f8(x, s)
+        bad = np.nonzero(got != ref)[0]
+        assert bad.size == 0, f"{bad.size} mismatches, e.g. x={x[bad[:4]]} gpu={got[bad[:4]]} ora={ref[bad[:4]]}"
+
+
+def test_quantize_input_nhwc4_bitexact(gpu):
+    from dlq_amd import ops
+    from dlq_amd.models import synthetic_images
+    x = synthetic_images(2, seed=5).numpy()
+    got = ops.quantize_nchw_to_nhwc_f8(_cuda(x), 0.0123).cpu().numpy()
+    ref = nchw_to_nhwc(O.quantize_f32_f8(x, 0.0123))
+    assert np.array_equal(got[..., :3], ref) and not got[..., 3].any()
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES, ids=[s[0] for s in CONV_SHAPES])
+@pytest.mark.parametrize("residual", [False, True])
+def test_conv_f8_within_one_step(gpu, shape, residual):
+    from dlq_amd import ops
+    name, IC, OC, k, s, p, H = shape
+    if residual and (IC == 3 or k == 1 or s == 2):
+        pytest.skip("stem / downsample / stride-2 conv1 take no residual (the API rejects one)")
+    rng = np.random.default_rng(17 + sum(map(ord, name)))
+    N = 2
+    x = O.quantize_f32_f8(np.abs(rng.standard_normal((N, IC, H, H))).astype(np.float32) * 40, 1.0)
+    w, bn = rand_conv(rng, OC, IC, k)
+    wq, sw = O.quantize_weights_f8(w)
+    s_x, s_y, s_r = 0.011, 0.013, 0.017
+    alpha, beta = O.fold_bn(s_x, sw, bn, s_y)
+    r_s = O.res_scale(s_r, s_y)
+    acc = O.conv_f8_acc(x, wq, s, p)
+    res = O.quantize_f32_f8(rng.standard_normal(acc.shape).astype(np.float32) * 50, 1.0) if residual else None
+    relu = k != 1
+    ref = O.epilogue_f8(acc, alpha, beta, res, r_s, relu)
+    c_store = 4 if IC == 3 else IC
+    xh = nchw_to_nhwc(x)
+    if c_store != IC:
+        xh = np.concatenate([xh, np.zeros(xh.shape[:3] + (c_store - IC,), np.uint8)], axis=3)
+    packed = ops.pack_conv_weights_f8(wq, c_store)
+    ocp = ops.packed_oc(OC)
+    y = ops.conv2d_nhwc_f8(_cuda(xh), _cuda(packed), OC, k, s, p, _cuda(ops.pad_vec(alpha, ocp)),
+                           _cuda(ops.pad_vec(beta, ocp)), residual=_cuda(nchw_to_nhwc(res)) if residual else None,
+                           res_scale=r_s, relu=relu)
+    got = nhwc_to_nchw(y.cpu().numpy())
+    assert got.shape == ref.shape
+    assert len(np.unique(ref)) > 50  # a real spread of codes, not a saturated tensor
+    s_abs = O.conv_f8_acc(x & 0x7F, wq & 0x7F, s, p)  # exact sum |w x|
+    err = 2.0 ** -16 * np.abs(alpha).astype(np.float64)[None, :, None, None] * s_abs
+    _check_conv(got, ref, err, 1e-3, name)
+
+
+def test_gap_and_fc_f8_bitexact(gpu):
+    from dlq_amd import ops
+    rng = np.random.default_rng(23)
+    x = O.quantize_f32_f8(np.abs(rng.standard_normal((5, 512, 7, 7))).astype(np.float32) * 30, 1.0)
+    k = O.gap_k_f8(0.02, 49, 0.015)
+    g_ref, _ = O.gap_f8(x, k)
+    g = ops.gap_nhwc_f8(_cuda(nchw_to_nhwc(x)), float(k)).cpu().numpy()
+    assert np.array_equal(g, g_ref)
+    w = rng.standard_normal((1000, 512)).astype(np.float32)
+    wq, sw = O.quantize_weights_f8(w)
+    bias = rng.standard_normal(1000).astype(np.float32)
+    al = O.fc_alpha(0.015, sw)
+    ref, _ = O.fc_f8(g_ref, wq, al, bias)
+    out = ops.linear_f8(_cuda(g_ref), _cuda(wq), _cuda(al), _cuda(bias)).cpu().numpy()
+    assert np.array_equal(out.view(np.int32), ref.view(np.int32))
+
+
+def test_resnet18_fp8_end_to_end(gpu):
+    from dlq_amd.models import ResNet18Int8, synthetic_images
+    sd, scales = model_and_scales_f8()
+    x = synthetic_images(2, seed=77).numpy()
+    ref_logits, dumps = O.resnet18_forward_f8(sd, scales, x)
+    model = ResNet18Int8(sd, scales, max_batch=4, keep_stages=True, precision="fp8")
+    logits = model(_cuda(x)).cpu().numpy()
+    torch.cuda.synchronize()
+    shapes = {"stem_pool": (56, 56, 64), "layer1": (56, 56, 64), "layer2": (28, 28, 128),
+              "layer3": (14, 14, 256), "layer4": (7, 7, 512)}
+    cosine = lambda a, b: float(np.dot(a.ravel(), b.ravel()) / np.linalg.norm(a) / np.linalg.norm(b))  # noqa: E731
+    worst = {}
+    for st, (h, w, c) in shapes.items():
+        got = nhwc_to_nchw(model.stage(st, (2, h, w, c)).cpu().numpy().view(np.uint8))
+        n = np.count_nonzero(got != dumps[st])
+        cs = cosine(O.decode_f8(got).astype(np.float64), O.decode_f8(dumps[st]).astype(np.float64))
+        print(f"{st}: {n / got.size:.4%} codes differ, decoded cosine vs oracle {cs:.6f}")
+        worst[st] = (n / got.size, cs)
+    for i in range(2):
+        f, _ = O.resnet18_forward_f32(sd, x[i])
+        cg = cosine(logits[i].astype(np.float64), f.astype(np.float64))
+        co = cosine(logits[i].astype(np.float64), ref_logits[i].astype(np.float64))
+        print(f"logits[{i}]: cosine vs fp32 reference {cg:.6f}, vs oracle fp8 {co:.6f}")
+        worst[f"logits{i}"] = (cg, co)
+    assert worst["stem_pool"][0] <= 0.01, worst
+    assert all(v[1] >= 0.99 for k, v in worst.items() if not k.startswith("logits")), worst
+    assert all(worst[f"logits{i}"][0] >= 0.995 for i in range(2)), worst
+
+
+def test_resnet18_fp8_batch_256_rows_independent(gpu):
+    """Full bench batch: rows 0 and 255 equal the same images run alone."""
+    from dlq_amd.models import ResNet18Int8, synthetic_images
+    sd, scales = model_and_scales_f8()
+    x = synthetic_images(256, seed=9).cuda()
+    model = ResNet18Int8(sd, scales, max_batch=256, precision="fp8")
+    full = model(x).cpu().numpy()
+    pair = model(x[[0, 255]].contiguous()).cpu().numpy()
+    assert np.array_equal(full[[0, 255]], pair)
+    assert np.isfinite(full).all()

@@ -38,6 +38,8 @@ PREFIX = [("stem_fused_kernel", 0), ("block_l1_kernel", 1), ("conv3x3s1_kernel",
 
 def family_of(kernel_name):
     n = kernel_name.replace("void ", "").replace("dlq::(anonymous namespace)::", "")
+    if n.startswith("conv_s8_kernel") and ", true>" in n:  # the F8 instantiations
+        return 7
     for p, f in PREFIX:
         if n.startswith(p):
             return f
