@@ -106,7 +106,13 @@ __device__ __forceinline__ void wave_tiles(int wave, int& mt, int& f0, int& nf) 
 // tile between the pair by taps, and 12 waves (3 per SIMD); fully contiguous
 // patch pieces -- what a channel-slice-major activation layout would give --
 // measured only 2-5 % faster, and no DMA at all 10-15 %).
-template <int W, int C, int OUT, bool RES, int NF, int NLD>
+// F8: e4m3 operands (the fp8 path).  The staged bytes are the
+// same; each v_mfma_f32_32x32x64_f8f6f4 takes TWO taps of the 32-channel slice
+// (bytes 0-15 tap 2p, 16-31 tap 2p+1, tap 8 paired with zeros: 5 MFMAs per
+// slice at twice the i8 MFMA's cycles, 10/9 of the int8 MFMA time), B
+// fragments stream through a 3-deep register ring (the doubled fragment
+// would not fit next to the fp32 accumulators otherwise).
+template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false>
 __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int mt, int f0, int lrank) {
   using G = IGeo<W>;
   constexpr int H = W, NS = C / ISC;
@@ -205,7 +211,8 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     col_off[0][f] = ow == 0 ? G::OFF_Z + ((bu - 1) & 15) * 16 : mid - 16;
     col_off[2][f] = ow == W - 1 ? G::OFF_Z + ((bu + 1) & 15) * 16 : mid + 16;
   }
-  v16i acc[NF];
+  using Acc = typename std::conditional<F8, v16f, v16i>::type;
+  Acc acc[NF];
   v4i rq[NF];
   int cur_ot = 0, cur_p0 = 0;
 
@@ -232,7 +239,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     if (j == 0) {
       item_of(li, cur_ot, cur_p0);
 #pragma unroll
-      for (int f = 0; f < NF; ++f) acc[f] = v16i{0};
+      for (int f = 0; f < NF; ++f) acc[f] = Acc{0};
     }
     const bool dma = more && loader && !(a.dbg & 2);
     const int sb = (s & 1) * G::SLOT;
@@ -248,6 +255,50 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
         col_off[2][f] += d;
       }
     }
+    if constexpr (F8) {
+      constexpr int NPAIR = 5, NM = NPAIR * NF, D = 3;
+      auto ld_half = [&](int tap, int f) -> v4i {
+        return *(const v4i*)(lds + col_off[tap % 3][f] + (tap / 3) * G::RW * 16);
+      };
+      auto ld_a2 = [&](int pr) -> v8i {
+        const v4i lo = *(const v4i*)(abase + (2 * pr) * 32);
+        const v4i hi = 2 * pr + 1 < 9 ? *(const v4i*)(abase + (2 * pr + 1) * 32) : v4i{0, 0, 0, 0};
+        return cat8(lo, hi);
+      };
+      auto ld_b2 = [&](int i) -> v8i {
+        const int pr = i / NF, f = i - pr * NF;
+        const v4i lo = ld_half(2 * pr, f);
+        const v4i hi = 2 * pr + 1 < 9 ? ld_half(2 * pr + 1, f) : v4i{0, 0, 0, 0};
+        return cat8(lo, hi);
+      };
+      v8i fa2[2], fbr[D];
+      fa2[0] = ld_a2(0);
+#pragma unroll
+      for (int i = 0; i < D; ++i) fbr[i] = ld_b2(i);
+#pragma unroll
+      for (int pr = 0; pr < NPAIR; ++pr) {
+        if (pr + 1 < NPAIR) fa2[(pr + 1) & 1] = ld_a2(pr + 1);
+        const int k0 = 2 * pr * DPW / 9, k1 = (2 * pr + 2 < 9 ? 2 * pr + 2 : 9) * DPW / 9;
+        if (dma) {
+#pragma unroll
+          for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          const int i = pr * NF + f;
+          acc[f] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa2[pr & 1], fbr[i % D], acc[f], 0, 0, 0, 0, 0, 0);
+          if (i + D < NM) fbr[i % D] = ld_b2(i + D);
+          if constexpr (OUT == 0 && RES) {
+            if (pr == NPAIR - 1 && j == NS - 1) {
+              const int p = cur_p0 + (f0 + f) * 32 + lr;
+              const bool keep = (f0 + f) * 32 + lr < IL && p < a.P;
+              const size_t off = keep ? (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16 : 0;
+              rq[f] = gload16_untracked(a.res + off);
+            }
+          }
+        }
+      }
+    } else {
     // A double-buffered per tap; each B fragment is re-loaded for the next
     // tap right after the MFMA that consumed it (one register set per tile).
     v4i fa[2], fb[NF];
@@ -298,6 +349,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
         __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
       }
     }
+    }  // int8 MFMA loop
 
     ISTAMP(2 + 2 * s);
     if (j != NS - 1) continue;
@@ -311,11 +363,15 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
         for (int g = 0; g < 4; ++g) {
           const int oc = cur_ot * G::OT + mt * 32 + 8 * g + 4 * lh;
           v4i* dst = keep ? (v4i*)((int*)a.y + (size_t)p * a.OC + oc) : (v4i*)(g_trash_i + lane * 16);
-          *dst = v4i{acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
+          if constexpr (F8)  // raw fp32 accumulators
+            *dst = v4i{__float_as_int(acc[f][4 * g]), __float_as_int(acc[f][4 * g + 1]),
+                       __float_as_int(acc[f][4 * g + 2]), __float_as_int(acc[f][4 * g + 3])};
+          else
+            *dst = v4i{acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
         }
       }
     } else {
-      const float lo = a.relu ? 0.f : -127.f;
+      const float lo = a.relu ? 0.f : (F8 ? -448.f : -127.f);
       float al[4][4], be[4][4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -345,11 +401,19 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
         unsigned q[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int ac[4] = {acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
-          if constexpr (RES)
-            q[g] = epi4_res(ac, al[g], be[g], rg[g], a.s_res, lo);
-          else
-            q[g] = epi4(ac, al[g], be[g], lo);
+          if constexpr (F8) {
+            const float ac[4] = {acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
+            if constexpr (RES)
+              q[g] = epi4_res_f8(ac, al[g], be[g], rg[g], a.s_res, lo);
+            else
+              q[g] = epi4_f8(ac, al[g], be[g], lo);
+          } else {
+            const int ac[4] = {acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
+            if constexpr (RES)
+              q[g] = epi4_res(ac, al[g], be[g], rg[g], a.s_res, lo);
+            else
+              q[g] = epi4(ac, al[g], be[g], lo);
+          }
         }
         swap32(q[0], q[2]);
         swap32(q[1], q[3]);
@@ -366,7 +430,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   ISTAMP(63);
 }
 
-template <int W, int C, int OUT, bool RES>
+template <int W, int C, int OUT, bool RES, bool F8 = false>
 __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   using G = IGeo<W>;
   constexpr int OFF_AB = G::OFF_AB;
@@ -390,14 +454,14 @@ __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   wave_tiles<G::MT>(wave, mt, f0, nf);
   if constexpr (G::MT == 4) {
     if (nf == 7)
-      conv3x3i_body<W, C, OUT, RES, 7, 8>(a, lds, mt, f0, wave);
+      conv3x3i_body<W, C, OUT, RES, 7, 8, F8>(a, lds, mt, f0, wave);
     else
-      conv3x3i_body<W, C, OUT, RES, 6, 8>(a, lds, mt, f0, wave);
+      conv3x3i_body<W, C, OUT, RES, 6, 8, F8>(a, lds, mt, f0, wave);
   } else {
     if (nf == 4)
-      conv3x3i_body<W, C, OUT, RES, 4, 8>(a, lds, mt, f0, wave);
+      conv3x3i_body<W, C, OUT, RES, 4, 8, F8>(a, lds, mt, f0, wave);
     else
-      conv3x3i_body<W, C, OUT, RES, 3, 8>(a, lds, mt, f0, wave);
+      conv3x3i_body<W, C, OUT, RES, 3, 8, F8>(a, lds, mt, f0, wave);
   }
 }
 
@@ -412,21 +476,32 @@ int num_cus_i() {
   return n;
 }
 
-template <int W, int C>
+template <int W, int C, bool F8 = false>
 hipError_t launch_ci(const ConvArgs& a, hipStream_t s) {
   using G = IGeo<W>;
   const int NI = (a.OCp / G::OT) * ((a.P + IL - 1) / IL), ncu = num_cus_i();
   const dim3 grid(NI < ncu ? NI : ncu), block(INW * 64);
   if (a.out_kind == 2)
-    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 2, false>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 2, false, F8>), grid, block, 0, s, a);
   else if (a.res)
-    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, true>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, true, F8>), grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, false>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, false, F8>), grid, block, 0, s, a);
   return hipGetLastError();
 }
 
 }  // namespace
+
+// e4m3 operands, same shapes and weight image layout (conv3x3w_pack of the codes).
+hipError_t launch_conv3x3i_f8(const ConvArgs& a, hipStream_t s) {
+  if (a.OCp != a.OC || a.C != a.OC || a.H != a.W) return hipErrorInvalidValue;
+  switch (a.W) {
+    case 28: return a.C == 128 ? launch_ci<28, 128, true>(a, s) : hipErrorInvalidValue;
+    case 14: return a.C == 256 ? launch_ci<14, 256, true>(a, s) : hipErrorInvalidValue;
+    case 7: return a.C == 512 ? launch_ci<7, 512, true>(a, s) : hipErrorInvalidValue;
+  }
+  return hipErrorInvalidValue;
+}
 
 // Same shapes and the same packed weight image as conv3x3w (conv3x3w_pack).
 hipError_t launch_conv3x3i(const ConvArgs& a, hipStream_t s) {

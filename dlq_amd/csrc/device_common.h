@@ -92,6 +92,25 @@ __device__ __forceinline__ unsigned enc4_f8(float y0, float y1, float y2, float 
   return (unsigned)r;
 }
 
+// e4m3 twins of epi4 / epi4_res on fp32 accumulators (packed fmas, then
+// enc4_f8): per element the same IEEE sequence as the generic fp8 kernel.
+__device__ __forceinline__ unsigned epi4_f8(const float* acc, const float* al, const float* be, float lo) {
+  const v2f y01 = __builtin_elementwise_fma(v2f{acc[0], acc[1]}, v2f{al[0], al[1]}, v2f{be[0], be[1]});
+  const v2f y23 = __builtin_elementwise_fma(v2f{acc[2], acc[3]}, v2f{al[2], al[3]}, v2f{be[2], be[3]});
+  return enc4_f8(y01[0], y01[1], y23[0], y23[1], lo);
+}
+__device__ __forceinline__ unsigned epi4_res_f8(const float* acc, const float* al, const float* be, unsigned r4,
+                                                float r_s, float lo) {
+  const v2f s = {r_s, r_s};
+  v2f y01 = __builtin_elementwise_fma(v2f{acc[0], acc[1]}, v2f{al[0], al[1]}, v2f{be[0], be[1]});
+  v2f y23 = __builtin_elementwise_fma(v2f{acc[2], acc[3]}, v2f{al[2], al[3]}, v2f{be[2], be[3]});
+  y01 = __builtin_elementwise_fma(
+      v2f{__builtin_amdgcn_cvt_f32_fp8((int)r4, 0), __builtin_amdgcn_cvt_f32_fp8((int)r4, 1)}, s, y01);
+  y23 = __builtin_elementwise_fma(
+      v2f{__builtin_amdgcn_cvt_f32_fp8((int)r4, 2), __builtin_amdgcn_cvt_f32_fp8((int)r4, 3)}, s, y23);
+  return enc4_f8(y01[0], y01[1], y23[0], y23[1], lo);
+}
+
 // Bijective XCD-aware remap: consecutive logical tiles land on one XCD
 // (cdna_hip_programming.md §5 "XCD swizzle must be bijective").
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

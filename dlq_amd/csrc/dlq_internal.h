@@ -83,6 +83,13 @@ hipError_t launch_im2col_nchw(const int8_t* x, int N, int C, int H, int W, int k
 // fp8 (e4m3) path (kernels.hip conv_s8_kernel<..., F8>, fp8.hip): generic
 // packed layout only.
 hipError_t launch_conv_f8(const ConvArgs& a, hipStream_t s);
+// conv3x3i with e4m3 operands (wide stride-1 shapes, conv3x3w_pack image).
+hipError_t launch_conv3x3i_f8(const ConvArgs& a, hipStream_t s);
+// fp8 weight image choice: the wide layout for conv3x3w_shape, else generic.
+bool f8_wide(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW);
+size_t packed_bytes_f8(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW);
+void pack_conv_weights_f8(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW,
+                          const uint8_t* q_oihw, int IC, uint8_t* packed);
 uint8_t f8_encode_host(float y);
 uint8_t f8_requant_host(float y, float lo);
 void quantize_weights_f8(const float* w, int OC, int K, uint8_t* q, float* scale);

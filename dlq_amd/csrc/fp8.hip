@@ -15,6 +15,7 @@
 // so both are bit-identical to the oracle; only the convs' fp32 MFMA
 // accumulation is inexact (tests/test_gpu_f8.py states the tolerance).
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/dlq.h"
@@ -186,6 +187,26 @@ uint8_t f8_requant_host(float y, float lo) {
   return f8_encode_host(y + 0.0f);
 }
 
+// DLQ_F8_GENERIC=1 (read at every call: a test switch) keeps every fp8 conv
+// on the generic kernel and layout.
+bool f8_wide(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW) {
+  const char* e = std::getenv("DLQ_F8_GENERIC");
+  return !(e && e[0] == '1') && conv3x3w_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW);
+}
+
+size_t packed_bytes_f8(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW) {
+  if (f8_wide(C, OC, H, W, kH, kW, sH, sW, pH, pW)) return conv3x3w_packed_bytes(OC, C);
+  return packed_bytes(OC, C, kH, kW);
+}
+
+void pack_conv_weights_f8(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW,
+                          const uint8_t* q, int IC, uint8_t* packed) {
+  if (f8_wide(C, OC, H, W, kH, kW, sH, sW, pH, pW))
+    conv3x3w_pack((const int8_t*)q, OC, IC, C, (int8_t*)packed);
+  else
+    pack_conv_weights((const int8_t*)q, OC, IC, kH, kW, C, (int8_t*)packed);
+}
+
 void quantize_weights_f8(const float* w, int OC, int K, uint8_t* q, float* scale) {
   for (int o = 0; o < OC; ++o) {
     float mx = 0.f;
@@ -235,12 +256,16 @@ int dlq_quantize_nchw_to_nhwc_f8(const float* x, int N, int C, int H, int W, int
   return launch_result("quantize_nchw_to_nhwc_f8");
 }
 
-size_t dlq_conv_packed_bytes_f8(const dlq_conv_desc* d) { return d ? packed_bytes(d->OC, d->C, d->kH, d->kW) : 0; }
+#define F8_GEOM(d) (d)->C, (d)->OC, (d)->H, (d)->W, (d)->kH, (d)->kW, (d)->sH, (d)->sW, (d)->pH, (d)->pW
+
+size_t dlq_conv_packed_bytes_f8(const dlq_conv_desc* d) {
+  return d && d->C > 0 && d->OC > 0 ? packed_bytes_f8(F8_GEOM(d)) : 0;
+}
 
 int dlq_pack_conv_weights_f8(const dlq_conv_desc* d, const uint8_t* q, int IC, uint8_t* packed) {
-  if (!d || !q || !packed || IC <= 0 || IC > d->C || packed_bytes(d->OC, d->C, d->kH, d->kW) == 0)
+  if (!d || !q || !packed || IC <= 0 || IC > d->C || d->OC <= 0 || packed_bytes_f8(F8_GEOM(d)) == 0)
     return fail(DLQ_ERR_ARG, "pack_conv_weights_f8: unsupported shape (need C%64==0 or the 7x7 C=4 stem)");
-  pack_conv_weights((const int8_t*)q, d->OC, IC, d->kH, d->kW, d->C, (int8_t*)packed);
+  pack_conv_weights_f8(F8_GEOM(d), q, IC, packed);
   return DLQ_OK;
 }
 
@@ -248,27 +273,29 @@ int dlq_conv2d_nhwc_f8(const dlq_conv_desc* d, const uint8_t* x, const uint8_t* 
                        const float* beta, const uint8_t* residual, float res_scale, int relu, uint8_t* y,
                        void* stream) {
   if (!d || !alpha || !beta) return fail(DLQ_ERR_ARG, "conv2d_f8: null pointer");
-  if (d->C <= 0 || d->OC <= 0 || packed_bytes(d->OC, d->C, d->kH, d->kW) == 0)
+  if (d->C <= 0 || d->OC <= 0 || packed_bytes_f8(F8_GEOM(d)) == 0)
     return fail(DLQ_ERR_ARG, "conv2d_f8: unsupported C (need C%64==0, or C==4 with a 7x7 kernel)");
   ConvArgs a;
   int rc = conv_args_checked(d, (const int8_t*)x, (const int8_t*)w_packed, alpha, beta, (const int8_t*)residual,
                              res_scale, relu, DLQ_OUT_S8, y, a);
   if (rc) return rc;
   if (a.P == 0) return DLQ_OK;
-  const hipError_t e = launch_conv_f8(a, (hipStream_t)stream);
+  const hipError_t e = f8_wide(F8_GEOM(d)) ? launch_conv3x3i_f8(a, (hipStream_t)stream)
+                                           : launch_conv_f8(a, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d_f8 launch: ") + hipGetErrorString(e));
 }
 
 int dlq_conv2d_nhwc_f8_acc(const dlq_conv_desc* d, const uint8_t* x, const uint8_t* w_packed, float* acc,
                            void* stream) {
-  if (!d || d->C <= 0 || d->OC <= 0 || packed_bytes(d->OC, d->C, d->kH, d->kW) == 0)
+  if (!d || d->C <= 0 || d->OC <= 0 || packed_bytes_f8(F8_GEOM(d)) == 0)
     return fail(DLQ_ERR_ARG, "conv2d_f8_acc: unsupported shape (need C%64==0, or C==4 with a 7x7 kernel)");
   ConvArgs a;
   int rc = conv_args_checked(d, (const int8_t*)x, (const int8_t*)w_packed, nullptr, nullptr, nullptr, 0.f, 0,
                              DLQ_OUT_S32, acc, a);
   if (rc) return rc;
   if (a.P == 0) return DLQ_OK;
-  const hipError_t e = launch_conv_f8(a, (hipStream_t)stream);
+  const hipError_t e = f8_wide(F8_GEOM(d)) ? launch_conv3x3i_f8(a, (hipStream_t)stream)
+                                           : launch_conv_f8(a, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d_f8_acc launch: ") + hipGetErrorString(e));
 }
 

@@ -611,8 +611,8 @@ int prepare_f8(dlq_resnet18* m, int max_batch) {
     std::vector<uint8_t> q((size_t)c.OC * K);
     std::vector<float> sw(c.OC);
     quantize_weights_f8(w.data(), c.OC, K, q.data(), sw.data());
-    std::vector<int8_t> packed(packed_bytes(c.OC, c.Cstore, c.k, c.k));
-    pack_conv_weights((const int8_t*)q.data(), c.OC, c.IC, c.k, c.k, c.Cstore, packed.data());
+    std::vector<uint8_t> packed(packed_bytes_f8(c.Cstore, c.OC, c.H, c.H, c.k, c.k, c.s, c.s, c.p, c.p));
+    pack_conv_weights_f8(c.Cstore, c.OC, c.H, c.H, c.k, c.k, c.s, c.s, c.p, c.p, q.data(), c.IC, packed.data());
     std::vector<float> alpha(ocp, 0.f), beta(ocp, 0.f);
     fold_bn(m->scales.at(c.in_site), sw.data(), m->tensors.at(c.bn + ".weight").data(),
             m->tensors.at(c.bn + ".bias").data(), m->tensors.at(c.bn + ".running_mean").data(),
@@ -793,7 +793,8 @@ namespace {
 // fp8 conv launch (generic implicit-GEMM kernel, e4m3 in and out).
 int conv_f8(dlq_resnet18* m, const ConvLayer& c, const int8_t* x, int N, int H, const int8_t* residual,
             float s_res, bool relu, int8_t* y, hipStream_t s) {
-  int rc = mark(m, s, DLQ_FAM_F8);
+  const bool wide = f8_wide(c.Cstore, c.OC, H, H, c.k, c.k, c.s, c.s, c.p, c.p);
+  int rc = mark(m, s, wide ? DLQ_FAM_WIDE : DLQ_FAM_F8);
   if (rc) return rc;
   dlq_conv_desc d{N, H, H, c.Cstore, c.OC, c.k, c.k, c.s, c.s, c.p, c.p};
   const float r_s = residual ? dlq::res_scale(s_res, m->scales.at(c.site)) : 0.f;
@@ -1003,15 +1004,18 @@ int dlq_resnet18_timing(dlq_resnet18* m, double* ms, int* launches, int* forward
 int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes) {
   if (!m || !macs || !bytes) return fail(DLQ_ERR_ARG, "family_work: null");
   for (int f = 0; f < DLQ_FAM_COUNT; ++f) macs[f] = bytes[f] = 0.0;
-  if (m->prec == DLQ_PREC_FP8) {  // every conv is one conv_s8_kernel<F8> launch
+  if (m->prec == DLQ_PREC_FP8) {  // one launch per conv: conv3x3i<F8> (wide) or conv_s8_kernel<F8>
+    auto fam = [&](const ConvLayer& c) {
+      return f8_wide(c.Cstore, c.OC, c.H, c.H, c.k, c.k, c.s, c.s, c.p, c.p) ? DLQ_FAM_WIDE : DLQ_FAM_F8;
+    };
     for (const ConvLayer& c : m->convs) {
       const int OH = out_dim(c.H, c.k, c.s, c.p);
-      macs[DLQ_FAM_F8] += (double)c.OC * c.IC * c.k * c.k * OH * OH;
-      bytes[DLQ_FAM_F8] += (double)c.H * c.H * c.Cstore + (double)OH * OH * c.OC;
+      macs[fam(c)] += (double)c.OC * c.IC * c.k * c.k * OH * OH;
+      bytes[fam(c)] += (double)c.H * c.H * c.Cstore + (double)OH * OH * c.OC;
     }
     for (const Block& b : m->blocks) {  // conv2's residual read
       const ConvLayer& c2 = m->convs[b.c2];
-      bytes[DLQ_FAM_F8] += (double)c2.H * c2.H * c2.OC;
+      bytes[fam(c2)] += (double)c2.H * c2.H * c2.OC;
     }
     macs[DLQ_FAM_FC] = 512.0 * 1000;
     bytes[DLQ_FAM_FC] = 512.0 + 4000.0;

@@ -301,11 +301,13 @@ def quantize_nchw_to_nhwc_f8(x: torch.Tensor, scale: float, c_out: int = 4) -> t
     return y
 
 
-def pack_conv_weights_f8(q_oihw: np.ndarray, C_store: int) -> np.ndarray:
-    """Generic packed image of e4m3 OIHW codes (dlq_pack_conv_weights_f8)."""
+def pack_conv_weights_f8(q_oihw: np.ndarray, C_store: int, H: int, stride: int, pad: int) -> np.ndarray:
+    """Packed image of e4m3 OIHW codes for the conv {H x H, stride, pad}
+    (dlq_pack_conv_weights_f8: the wide layout for the layer2-4 stride-1 3x3
+    shapes, the generic one otherwise)."""
     q = np.ascontiguousarray(q_oihw, np.uint8)
     OC, IC, k, _ = q.shape
-    d = ConvDesc(1, 1, 1, C_store, OC, k, k, 1, 1, 0, 0)
+    d = ConvDesc(1, H, H, C_store, OC, k, k, stride, stride, pad, pad)
     nb = lib.dlq_conv_packed_bytes_f8(C.byref(d))
     if nb == 0:
         raise ValueError("unsupported conv shape for the fp8 path")

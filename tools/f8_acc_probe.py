@@ -38,10 +38,12 @@ def emulate(x, w, s, p):
 def main():
     rng = np.random.default_rng(5)
     res = {}
-    for (Cc, OC, k, s, p, H) in [(256, 128, 3, 1, 1, 14), (128, 128, 3, 1, 1, 28), (512, 128, 3, 1, 1, 7)]:
+    tag = "_generic" if os.environ.get("DLQ_F8_GENERIC") == "1" else ""
+    for (Cc, OC, k, s, p, H) in [(256, 128, 3, 1, 1, 14), (128, 128, 3, 1, 1, 28), (512, 128, 3, 1, 1, 7),
+                                 (256, 256, 3, 1, 1, 14)]:
         x = O.quantize_f32_f8(np.abs(rng.standard_normal((1, Cc, H, H))).astype(np.float32) * 40, 1.0)
         w = O.quantize_f32_f8(rng.standard_normal((OC, Cc, k, k)).astype(np.float32) * 60, 1.0)
-        packed = ops.pack_conv_weights_f8(w, Cc)
+        packed = ops.pack_conv_weights_f8(w, Cc, H, s, p)
         xh = np.ascontiguousarray(np.transpose(x, (0, 2, 3, 1)))
         acc = ops.conv2d_nhwc_f8_acc(torch.from_numpy(xh).cuda(), torch.from_numpy(packed).cuda(), OC, k, s, p)
         got = np.transpose(acc.cpu().numpy(), (0, 3, 1, 2)).astype(np.float32)
@@ -53,7 +55,7 @@ def main():
         for d in dots:
             a1 = (a1.astype(np.float64) + d).astype(np.float32)
             a2 = (a2 + d.astype(np.float32)).astype(np.float32)
-        key = f"C{Cc}_H{H}"
+        key = f"C{Cc}_OC{OC}_H{H}{tag}"
         res[key] = {"n": int(got.size),
                     "eq_exact": int(np.count_nonzero(got == h_exact)),
                     "eq_step_fused": int(np.count_nonzero(got == a1)),
@@ -62,7 +64,7 @@ def main():
         np.savez_compressed(f"gpurun_out/f8_probe_{key}.npz", x=x, w=w, got=got)
         print(key, res[key], flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
-    json.dump(res, open("gpurun_out/f8_acc_probe.json", "w"), indent=1)
+    json.dump(res, open(f"gpurun_out/f8_acc_probe{tag}.json", "w"), indent=1)
 
 
 if __name__ == "__main__":
