@@ -67,7 +67,8 @@ hipError_t launch_block_l1(const int8_t* x, int N, const int8_t* w1, const float
 size_t stem_packed_bytes();
 void pack_stem_weights(const int8_t* q_oihw, const float* alpha, int8_t* out, float* alpha_abs);
 hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float* alpha, const float* beta,
-                             float inv_s, int8_t* y, hipStream_t s);
+                             float inv_s, int8_t* y, hipStream_t s, bool f8 = false);
+void pack_stem_weights_f8(const uint8_t* q_oihw, const float* alpha, uint8_t* out, float* alpha_abs);
 hipError_t launch_quantize_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cout,
                                         float inv_s, int8_t* y, hipStream_t s);
 hipError_t launch_quantize_rows(const float* x, int rows, int cols, int ldy, float inv_s,

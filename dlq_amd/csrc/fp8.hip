@@ -299,6 +299,23 @@ int dlq_conv2d_nhwc_f8_acc(const dlq_conv_desc* d, const uint8_t* x, const uint8
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d_f8_acc launch: ") + hipGetErrorString(e));
 }
 
+int dlq_pack_stem_weights_f8(const uint8_t* q_oihw, const float* alpha, uint8_t* packed, float* alpha_packed) {
+  if (!q_oihw || !alpha || !packed || !alpha_packed) return fail(DLQ_ERR_ARG, "pack_stem_weights_f8: null");
+  pack_stem_weights_f8(q_oihw, alpha, packed, alpha_packed);
+  return DLQ_OK;
+}
+
+int dlq_stem_fused_f8(const float* x, int N, const uint8_t* w_stem, const float* alpha, const float* beta,
+                      float inv_s, uint8_t* y, void* stream) {
+  if (N < 0) return fail(DLQ_ERR_ARG, "stem_fused_f8: bad batch");
+  if (N == 0) return DLQ_OK;
+  if (!x || !w_stem || !alpha || !beta || !y) return fail(DLQ_ERR_ARG, "stem_fused_f8: null pointer");
+  if ((long long)N * 3 * 224 * 224 * 4 >= (1LL << 31) * 4LL) return fail(DLQ_ERR_ARG, "stem_fused_f8: batch too large");
+  const hipError_t e =
+      launch_stem_fused(x, N, (const int8_t*)w_stem, alpha, beta, inv_s, (int8_t*)y, (hipStream_t)stream, true);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("stem_fused_f8 launch: ") + hipGetErrorString(e));
+}
+
 int dlq_gap_nhwc_f8(const uint8_t* x, int N, int C, int HW, float k, uint8_t* y, void* stream) {
   if (N < 0 || C <= 0 || C % 4 || HW <= 0) return fail(DLQ_ERR_ARG, "gap_f8: bad shape (C % 4 == 0)");
   if (N == 0) return DLQ_OK;

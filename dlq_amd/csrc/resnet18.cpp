@@ -621,6 +621,13 @@ int prepare_f8(dlq_resnet18* m, int max_batch) {
     if ((rc = upload(m, &c.w, packed.data(), packed.size())) || (rc = upload(m, &c.alpha, alpha.data(), ocp * 4)) ||
         (rc = upload(m, &c.beta, beta.data(), ocp * 4)))
       return rc;
+    if (&c == &m->convs[m->stem]) {  // the fused stem's image (sign bits of alpha < 0 rows flipped)
+      std::vector<uint8_t> sp(stem_packed_bytes());
+      std::vector<float> sa(64);
+      pack_stem_weights_f8(q.data(), alpha.data(), sp.data(), sa.data());
+      if ((rc = upload(m, &m->stem_w, sp.data(), sp.size())) || (rc = upload(m, &m->stem_alpha, sa.data(), 64 * 4)))
+        return rc;
+    }
   }
   {
     const int O = 1000, I = 512;
@@ -639,8 +646,9 @@ int prepare_f8(dlq_resnet18* m, int max_batch) {
       return rc;
   }
   const size_t B = (size_t)max_batch;
-  if ((rc = dev_alloc(m, &m->gq, B * 512)) || (rc = dev_alloc(m, &m->xq, B * 224 * 224 * kStemC)) ||
-      (rc = dev_alloc(m, &m->c1, B * 112 * 112 * 64)))
+  if ((rc = dev_alloc(m, &m->gq, B * 512))) return rc;
+  if (unfused_stem() &&
+      ((rc = dev_alloc(m, &m->xq, B * 224 * 224 * kStemC)) || (rc = dev_alloc(m, &m->c1, B * 112 * 112 * 64))))
     return rc;
   for (auto& b : m->buf)
     if ((rc = dev_alloc(m, &b, B * 56 * 56 * 64))) return rc;
@@ -808,17 +816,25 @@ int forward_pass_f8(dlq_resnet18* m, const float* x, int B, float* logits, hipSt
   const size_t nB = (size_t)B;
   int rc;
   const ConvLayer& st = m->convs[m->stem];
-  if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
-  rc = dlq_quantize_nchw_to_nhwc_f8(x, B, 3, 224, 224, kStemC, inv_scale(m->scales.at("input")), (uint8_t*)m->xq, s);
-  if (rc) return rc;
-  if (record) m->stage["input_q"] = {m->xq, nB * 224 * 224 * kStemC};
-  if ((rc = conv_f8(m, st, m->xq, B, 224, nullptr, 0.f, true, m->c1, s))) return rc;
-  if (record) m->stage["conv1"] = {m->c1, nB * 112 * 112 * 64};
   int ci = 0;
   int8_t* cur = m->buf[ci];
-  if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
-  // post-ReLU e4m3 codes are 0x00..0x7e: their int8 max is the value max
-  if ((rc = dlq_maxpool2d_3x3_s2p1_nhwc_s8(m->c1, B, 64, 112, 112, cur, s))) return rc;
+  if (!unfused_stem()) {
+    if ((rc = mark(m, s, DLQ_FAM_STEM))) return rc;
+    rc = dlq_stem_fused_f8(x, B, (const uint8_t*)m->stem_w, m->stem_alpha, st.beta, inv_scale(m->scales.at("input")),
+                           (uint8_t*)cur, s);
+    if (rc) return rc;
+  } else {
+    if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
+    rc = dlq_quantize_nchw_to_nhwc_f8(x, B, 3, 224, 224, kStemC, inv_scale(m->scales.at("input")), (uint8_t*)m->xq,
+                                      s);
+    if (rc) return rc;
+    if (record) m->stage["input_q"] = {m->xq, nB * 224 * 224 * kStemC};
+    if ((rc = conv_f8(m, st, m->xq, B, 224, nullptr, 0.f, true, m->c1, s))) return rc;
+    if (record) m->stage["conv1"] = {m->c1, nB * 112 * 112 * 64};
+    if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
+    // post-ReLU e4m3 codes are 0x00..0x7e: their int8 max is the value max
+    if ((rc = dlq_maxpool2d_3x3_s2p1_nhwc_s8(m->c1, B, 64, 112, 112, cur, s))) return rc;
+  }
   if (record && (rc = record_stage(m, "stem_pool", cur, nB * 56 * 56 * 64, s))) return rc;
   int H = 56;
   for (const Block& b : m->blocks) {
@@ -1010,6 +1026,11 @@ int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes)
     };
     for (const ConvLayer& c : m->convs) {
       const int OH = out_dim(c.H, c.k, c.s, c.p);
+      if (&c == &m->convs[m->stem] && !unfused_stem()) {  // fp32 input read + pooled e4m3 output
+        macs[DLQ_FAM_STEM] = (double)c.OC * c.IC * c.k * c.k * OH * OH;
+        bytes[DLQ_FAM_STEM] = 3.0 * 224 * 224 * 4 + 56.0 * 56 * 64;
+        continue;
+      }
       macs[fam(c)] += (double)c.OC * c.IC * c.k * c.k * OH * OH;
       bytes[fam(c)] += (double)c.H * c.H * c.Cstore + (double)OH * OH * c.OC;
     }

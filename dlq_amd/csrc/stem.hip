@@ -28,6 +28,9 @@
 // column quarters; quarter q computes conv columns 28q-1 .. 28q+30 (32, of
 // which 29 are used) and produces pooled columns 14q .. 14q+13.  A step
 // computes conv rows 2p, 2p+1 and emits pooled row p.
+#include <cmath>
+#include <type_traits>
+
 #include "device_common.h"
 
 namespace dlq {
@@ -86,7 +89,16 @@ __device__ __forceinline__ int max3i(int a, int b, int c) {
   return __builtin_elementwise_max(__builtin_elementwise_max(a, b), c);
 }
 
+// F8: the fp8 path: the input is quantised to e4m3 (enc4_f8),
+// the 8 i8 k-steps become 4 v_mfma_f32_32x32x64_f8f6f4 (k-steps 2i, 2i+1 as
+// the two halves of each 32-byte fragment, A and B alike), the pool runs on
+// the fp32 accumulators (max is exact; the e4m3 epilogue is monotone once
+// alpha >= 0: dlq_pack_stem_weights_f8 flips the sign bits of the rows with
+// alpha < 0).
+template <bool F8>
 __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
+  using Acc = typename std::conditional<F8, v16f, v16i>::type;
+  using Pv = typename std::conditional<F8, float, int>::type;
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_STEM];
   const unsigned lds32 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) int8_t*)lds;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -143,6 +155,17 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
       int2 out = {0, 0};
       if ((unsigned)sr < 112u && (unsigned)sc < 112u) {
         const int8_t* raw = lds + OFF_RAW + (k % RAW_SLOTS) * RAW_SLOT_BYTES + h * 6 * 1024 + sc * 8;
+        if constexpr (F8) {  // (c0, c1, c2, +0) e4m3 per pixel
+          float v[3][2];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int2 f = *(const int2*)(raw + (c * 2 + dy) * 1024);
+            v[c][0] = __int_as_float(f.x) * a.inv_s;
+            v[c][1] = __int_as_float(f.y) * a.inv_s;
+          }
+          out.x = (int)enc4_f8(v[0][0], v[1][0], v[2][0], 0.f, -448.f);
+          out.y = (int)enc4_f8(v[0][1], v[1][1], v[2][1], 0.f, -448.f);
+        } else {
         unsigned u[3][2];  // [c][dx]: clamp(x/s) + 1.5*2^23 -> rne'd int8 in the low byte
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -157,6 +180,7 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
           const unsigned t = __builtin_amdgcn_perm(u[1][dx], u[0][dx], 0x0c0c0400u);
           (dx ? out.y : out.x) = (int)__builtin_amdgcn_perm(u[2][dx], t, 0x0c040100u);
         }
+        }
       }
       *(int2*)(lds + OFF_PATCH + (sr & (PATCH_SLOTS - 1)) * PATCH_ROW + unit * 16 + dy * 8) = out;
     };
@@ -169,22 +193,37 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
         af[kk] = *(const v4i*)(lds + OFF_PATCH + (sr & (PATCH_SLOTS - 1)) * PATCH_ROW +
                                (a_unit + 2 * (kk & 1) + lh) * 16);
       }
-      v16i acc = v16i{0};
+      Acc acc = Acc{0};
+      if constexpr (F8) {
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[kk], wreg[kk], acc, 0, 0, 0);
+        for (int kp = 0; kp < 4; ++kp)
+          acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(cat8(af[2 * kp], af[2 * kp + 1]),
+                                                                cat8(wreg[2 * kp], wreg[2 * kp + 1]), acc, 0, 0, 0,
+                                                                0, 0, 0);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[kk], wreg[kk], acc, 0, 0, 0);
+      }
       return acc;
     };
+    auto mx3 = [](Pv x, Pv y, Pv z) -> Pv {
+      if constexpr (F8)
+        return __builtin_fmaxf(__builtin_fmaxf(x, y), z);
+      else
+        return max3i(x, y, z);
+    };
+    const Pv kLow = F8 ? (Pv)-INFINITY : (Pv)kIntMin;
     // Horizontal 3-max of a conv row, H[m] = max(local cols 2m, 2m+1, 2m+2):
     // half 0 takes column 16 from half 1; quarter 0's column 0 is conv column
     // -1 (pool padding).  Half 1's H[6], H[7] and half 0's beyond m=7 are unused.
-    auto hpool = [&](v16i c, int (&H)[8]) {
-      unsigned x0 = (unsigned)c[0], c16 = (unsigned)c[0];
+    auto hpool = [&](Acc c, Pv (&H)[8]) {
+      unsigned x0 = __builtin_bit_cast(unsigned, c[0]), c16 = x0;
       swap32(x0, c16);  // lanes 0-31: c16 = lanes 32-63's c[0]
-      const int c0v = (q == 0 && lh == 0) ? kIntMin : c[0];
-      H[0] = max3i(c0v, c[1], c[2]);
+      const Pv c0v = (q == 0 && lh == 0) ? kLow : c[0];
+      H[0] = mx3(c0v, c[1], c[2]);
 #pragma unroll
-      for (int m = 1; m < 7; ++m) H[m] = max3i(c[2 * m], c[2 * m + 1], c[2 * m + 2]);
-      H[7] = max3i(c[14], c[15], (int)c16);
+      for (int m = 1; m < 7; ++m) H[m] = mx3(c[2 * m], c[2 * m + 1], c[2 * m + 2]);
+      H[7] = mx3(c[14], c[15], __builtin_bit_cast(Pv, c16));
     };
 
     // ---- prologue: pairs 0 .. SLA in flight (the ring's SLA+1 slots);
@@ -202,10 +241,10 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
     __syncthreads();
     issue_pair(SLA + 1);
     issue_pair(SLA + 2);
-    int Hp[8];
+    Pv Hp[8];
     if (py0 == 0) {
 #pragma unroll
-      for (int m = 0; m < 8; ++m) Hp[m] = kIntMin;  // conv row -1: pool padding
+      for (int m = 0; m < 8; ++m) Hp[m] = kLow;  // conv row -1: pool padding
     } else {
       hpool(conv_row(2 * py0 - 1), Hp);
     }
@@ -234,18 +273,22 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
       issue_pair(t + 3 + SLA);
       ST(2);
 
-      int He[8], Ho[8];
+      Pv He[8], Ho[8];
       hpool(conv_row(2 * p), He);
       hpool(conv_row(2 * p + 1), Ho);
       ST(3);
       // vertical max, epilogue on the pooled values, bytes -> staging [16 px][32 oc]
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
-        const int v = max3i(Hp[m], He[m], Ho[m]);
+        const Pv v = mx3(Hp[m], He[m], Ho[m]);
         Hp[m] = Ho[m];
         const float y = __builtin_fmaf((float)v, al, be);
-        const unsigned u = __float_as_uint(__builtin_amdgcn_fmed3f(y, 0.f, 127.f) + 12582912.0f);
-        stg[(m + 8 * lh) * 32 + lr] = (int8_t)u;
+        if constexpr (F8) {
+          stg[(m + 8 * lh) * 32 + lr] = (int8_t)enc4_f8(y, 0.f, 0.f, 0.f, 0.f);
+        } else {
+          const unsigned u = __float_as_uint(__builtin_amdgcn_fmed3f(y, 0.f, 127.f) + 12582912.0f);
+          stg[(m + 8 * lh) * 32 + lr] = (int8_t)u;
+        }
       }
       // 14 pooled columns x 32 channels = 28 x 16 B, staged in LDS (written by
       // this wave: LDS is in order); stored during the next step
@@ -295,8 +338,28 @@ void pack_stem_weights(const int8_t* q, const float* alpha, int8_t* out, float* 
   }
 }
 
+// e4m3 twin: the sign bit is the negation.
+void pack_stem_weights_f8(const uint8_t* q, const float* alpha, uint8_t* out, float* alpha_abs) {
+  for (int i = 0; i < 64 * 256; ++i) out[i] = 0;
+  for (int o = 0; o < 64; ++o) {
+    const bool neg = alpha[o] < 0.f;
+    alpha_abs[o] = neg ? -alpha[o] : alpha[o];
+    for (int ky = 0; ky < 4; ++ky)
+      for (int kx = 0; kx < 4; ++kx)
+        for (int dy = 0; dy < 2; ++dy)
+          for (int dx = 0; dx < 2; ++dx) {
+            const int kh = 2 * ky + dy - 1, kw = 2 * kx + dx - 1;
+            if (kh < 0 || kw < 0) continue;
+            for (int c = 0; c < 3; ++c) {
+              const uint8_t v = q[((o * 3 + c) * 7 + kh) * 7 + kw];
+              out[o * 256 + (((ky * 4 + kx) * 2 + dy) * 2 + dx) * 4 + c] = neg ? (uint8_t)(v ^ 0x80) : v;
+            }
+          }
+  }
+}
+
 hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float* alpha, const float* beta,
-                             float inv_s, int8_t* y, hipStream_t s) {
+                             float inv_s, int8_t* y, hipStream_t s, bool f8) {
   const int ncu = num_cus_stem();
   int nb = (ncu + N - 1) / N;  // bands per image so that every CU gets an item
   nb = nb < 1 ? 1 : (nb > 14 ? 14 : nb);
@@ -304,7 +367,10 @@ hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float
   nb = (56 + R - 1) / R;
   StemArgs a{x, w, alpha, beta, y, inv_s, N, nb, R};
   const int items = N * nb;
-  hipLaunchKernelGGL(stem_fused_kernel, dim3(items < ncu ? items : ncu), dim3(SNW * 64), 0, s, a);
+  if (f8)
+    hipLaunchKernelGGL(stem_fused_kernel<true>, dim3(items < ncu ? items : ncu), dim3(SNW * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL(stem_fused_kernel<false>, dim3(items < ncu ? items : ncu), dim3(SNW * 64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -108,6 +108,8 @@ _SIGS = {
     "dlq_gap_nhwc_f8": ([_vp, _i, _i, _i, _f, _vp, _vp], _i),
     "dlq_linear_f8": ([_vp, _i, _i, _vp, _i, _vp, _vp, _vp, _vp], _i),
     "dlq_resnet18_set_precision": ([_vp, _i], _i),
+    "dlq_pack_stem_weights_f8": ([_vp, _vp, _vp, _vp], _i),
+    "dlq_stem_fused_f8": ([_vp, _i, _vp, _vp, _vp, _f, _vp, _vp], _i),
 }
 
 if not os.path.exists(LIB_PATH):

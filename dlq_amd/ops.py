@@ -357,3 +357,27 @@ def linear_f8(x: torch.Tensor, w: torch.Tensor, alpha: torch.Tensor, beta: torch
     y = torch.empty((N, O), dtype=torch.float32, device=x.device)
     check(lib.dlq_linear_f8(ptr(x), N, K, ptr(w), O, ptr(alpha), ptr(beta), ptr(y), stream_handle()), "linear_f8")
     return y
+
+
+def pack_stem_weights_f8(q_oihw: np.ndarray, alpha: np.ndarray):
+    q = np.ascontiguousarray(q_oihw, np.uint8)
+    a = np.ascontiguousarray(alpha, np.float32)
+    out = np.empty(64 * 256, np.uint8)
+    ap = np.empty(64, np.float32)
+    check(lib.dlq_pack_stem_weights_f8(q.ctypes.data, a.ctypes.data, out.ctypes.data, ap.ctypes.data),
+          "pack_stem_weights_f8")
+    return out, ap
+
+
+def stem_fused_f8(x: torch.Tensor, w_stem: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor,
+                  in_scale: float) -> torch.Tensor:
+    """e4m3 fused stem: fp32 NCHW [N,3,224,224] -> e4m3 NHWC [N,56,56,64]."""
+    _dev(x, torch.float32)
+    N = x.shape[0]
+    if tuple(x.shape[1:]) != (3, 224, 224):
+        raise ValueError(f"stem input must be [N,3,224,224], got {tuple(x.shape)}")
+    y = torch.empty((N, 56, 56, 64), dtype=torch.uint8, device=x.device)
+    inv = float(np.float32(1.0) / np.float32(in_scale))
+    check(lib.dlq_stem_fused_f8(ptr(x), N, ptr(w_stem), ptr(alpha), ptr(beta), inv, ptr(y), stream_handle()),
+          "stem_fused_f8")
+    return y

@@ -397,6 +397,13 @@ int dlq_conv2d_nhwc_f8(const dlq_conv_desc* d, const uint8_t* x, const uint8_t* 
  * NHWC [N][OH][OW][OC] fp32 (parity / debugging). */
 int dlq_conv2d_nhwc_f8_acc(const dlq_conv_desc* d, const uint8_t* x, const uint8_t* w_packed, float* acc,
                            void* stream);
+/* twin of dlq_pack_stem_weights_s8 / dlq_stem_fused_s8 (quantise + conv1 +
+ * BN/ReLU + maxpool in one launch; the rows of channels with alpha < 0 get
+ * their sign bits flipped).  Equal, within the conv bound, to
+ * dlq_quantize_nchw_to_nhwc_f8 + dlq_conv2d_nhwc_f8 (stem) + the maxpool. */
+int dlq_pack_stem_weights_f8(const uint8_t* q_oihw, const float* alpha, uint8_t* packed, float* alpha_packed);
+int dlq_stem_fused_f8(const float* x, int N, const uint8_t* w_stem, const float* alpha, const float* beta,
+                      float inv_s, uint8_t* y, void* stream);
 /* twin of dlq_gap_nhwc_s8: exact sum of the values in units of 2^-9, then
  * requant(float(sum) * k) with k = s_in/HW/s_out * 2^-9.  The int8
  * dlq_maxpool2d_3x3_s2p1_nhwc_s8 applies unchanged to non-negative e4m3. */

@@ -145,6 +145,44 @@ def _run_conv(shape, residual, N):
     _check_conv(got, ref, err, 3e-3, name)
 
 
+def _maxpool_f64(a):
+    """3x3/s2/p1 max over NCHW float64 (-inf padding)."""
+    N, Cc, H, W = a.shape
+    ap = np.pad(a, ((0, 0), (0, 0), (1, 1), (1, 1)), constant_values=-np.inf)
+    OH = (H + 2 - 3) // 2 + 1
+    out = np.full((N, Cc, OH, OH), -np.inf)
+    for kh in range(3):
+        for kw in range(3):
+            out = np.maximum(out, ap[:, :, kh:kh + 2 * OH:2, kw:kw + 2 * OH:2])
+    return out
+
+
+@pytest.mark.parametrize("N", [1, 3])
+def test_stem_fused_f8_within_bound(gpu, N):
+    """quantise + conv1 + BN/ReLU + maxpool in one launch vs the oracle's
+    separate steps; the pooled bound is the window max of the conv bound."""
+    from dlq_amd import ops
+    from dlq_amd.models import synthetic_images
+    rng = np.random.default_rng(41 + N)
+    x = synthetic_images(N, seed=100 + N).numpy()
+    w, bn = rand_conv(rng, 64, 3, 7)
+    wq, sw = O.quantize_weights_f8(w)
+    s_in, s_y = 0.0061, 0.0123
+    alpha, beta = O.fold_bn(s_in, sw, bn, s_y)
+    alpha[5] = -abs(alpha[5])  # a negative-alpha channel: the sign-flip packing path
+    xq = O.quantize_f32_f8(x, s_in)
+    acc = O.conv_f8_acc(xq, wq, 2, 3)
+    ref = O.maxpool_s8(O.epilogue_f8(acc, alpha, beta, relu=True).view(np.int8)).view(np.uint8)
+    s_abs = O.conv_f8_acc(xq & 0x7F, wq & 0x7F, 2, 3)
+    err = _maxpool_f64(2.0 ** -16 * np.abs(alpha).astype(np.float64)[None, :, None, None] * s_abs)
+    ws, ap = ops.pack_stem_weights_f8(wq, alpha)
+    y = ops.stem_fused_f8(_cuda(x), _cuda(ws), _cuda(ap), _cuda(beta), s_in)
+    got = nhwc_to_nchw(y.cpu().numpy())
+    assert got.shape == ref.shape
+    assert len(np.unique(ref)) > 50
+    _check_conv(got, ref, err, 3e-3, "stem")
+
+
 def test_gap_and_fc_f8_bitexact(gpu):
     from dlq_amd import ops
     rng = np.random.default_rng(23)
