@@ -39,6 +39,7 @@
 // fma(acc, a1, b1) -> ReLU -> rne -> int8 written to the intermediate ring;
 // conv2 y = fma(acc, a2, b2) + s_res * x -> ReLU -> rne -> int8 to HBM.
 #include <cstdlib>
+#include <type_traits>
 #include <utility>
 
 #include "device_common.h"
@@ -133,11 +134,22 @@ __device__ __forceinline__ void wait_lgkm_tie(v4i& x, v4i& y) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(x), "+v"(y) : "n"(N) : "memory");
 }
 template <int N>
+__device__ __forceinline__ void wait_lgkm_tie8(v8i& x, v8i& y) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(x), "+v"(y) : "n"(N) : "memory");
+}
+template <int N>
 __device__ __forceinline__ void wait_vm_tie(v4i& x, v4i& y) {
   asm volatile("s_waitcnt vmcnt(%2)" : "+v"(x), "+v"(y) : "n"(N) : "memory");
 }
 
+// F8: the fp8 path.  A tap's two 32-channel k-steps form one
+// 64-deep v_mfma_f32_32x32x64_f8f6f4 (A = the tap's two resident weight
+// fragments, B = the pixel's two channel-half fragments): 9 MFMAs per tile at
+// twice the i8 cycles = the int8 MFMA time; pixel fragments one tap ahead.
+// Epilogues: enc4_f8 with the residual decoded by v_cvt_f32_fp8.
+template <bool F8>
 __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
+  using Acc = typename std::conditional<F8, v16f, v16i>::type;
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: roles branch on SGPRs
@@ -228,9 +240,28 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
   // issues at the full rate); pixel fragments are read two k-steps ahead.
   // k-step ks = tap (kh, kw), channel half kk: row base ra[kh], immediate
   // offset 16*kw + kk*2 planes.
-  auto run_job = [&](const unsigned (&r0)[3], const unsigned (&r1)[3], v16i (&acc)[2]) {
-    acc[0] = v16i{0};
-    acc[1] = v16i{0};
+  auto run_job = [&](const unsigned (&r0)[3], const unsigned (&r1)[3], Acc (&acc)[2]) {
+    acc[0] = Acc{0};
+    acc[1] = Acc{0};
+    if constexpr (F8) {
+      v8i bq[2][2];
+      auto ld2 = [&](auto tc, int buf) {
+        constexpr int tap = decltype(tc)::value, kh = tap / 3, kw = tap % 3;
+        bq[buf][0] = cat8(ds_read16<16 * kw>(r0[kh]), ds_read16<16 * kw + 2 * PL>(r0[kh]));
+        bq[buf][1] = cat8(ds_read16<16 * kw>(r1[kh]), ds_read16<16 * kw + 2 * PL>(r1[kh]));
+      };
+      ld2(std::integral_constant<int, 0>{}, 0);
+      auto tstep = [&](auto tc) {
+        constexpr int tap = decltype(tc)::value;
+        if constexpr (tap + 1 < 9) ld2(std::integral_constant<int, tap + 1>{}, (tap + 1) & 1);
+        wait_lgkm_tie8<tap + 1 < 9 ? 4 : 0>(bq[tap & 1][0], bq[tap & 1][1]);
+        const v8i wa = cat8(wr[2 * tap], wr[2 * tap + 1]);
+        acc[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wa, bq[tap & 1][0], acc[0], 0, 0, 0, 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wa, bq[tap & 1][1], acc[1], 0, 0, 0, 0, 0, 0);
+      };
+      static_for<0, 9>(tstep);
+      return;
+    } else {
     v4i bf[3][2];
     auto ld = [&](auto nc, int buf) {
       constexpr int n = decltype(nc)::value, tap = n >> 1, kh = tap / 3, kw = tap % 3;
@@ -249,6 +280,7 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
       acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wr[ks], bf[ks % 3][1], acc[1], 0, 0, 0);
     };
     static_for<0, KS>(step);
+    }
   };
 
   // Epilogue of one 32 oc x 32 px tile in the MFMA layout (lane: pixel lr,
@@ -256,7 +288,27 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
   // of the pixel.  rs: the residual's 16 bytes in that store layout (conv2).
   // Pairs of elements go through v_pk_fma_f32 / v_pk_add_f32 (per-component
   // IEEE fma / add: bit-identical to the scalar sequence).
-  auto epilogue = [&](const v16i& acc, bool res, v4i rs) -> v4i {
+  auto epilogue = [&](const Acc& acc, bool res, v4i rs) -> v4i {
+    if constexpr (F8) {
+      unsigned rg[4] = {0, 0, 0, 0};
+      if (res) {  // store layout -> MFMA layout (e4m3 bytes, decoded below)
+        unsigned rr[4] = {(unsigned)rs[0], (unsigned)rs[1], (unsigned)rs[2], (unsigned)rs[3]};
+        swap32(rr[0], rr[1]);
+        swap32(rr[2], rr[3]);
+        rg[0] = rr[0];
+        rg[1] = rr[2];
+        rg[2] = rr[1];
+        rg[3] = rr[3];
+      }
+      unsigned qv[4];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float ac[4] = {acc[4 * g4], acc[4 * g4 + 1], acc[4 * g4 + 2], acc[4 * g4 + 3]};
+        qv[g4] = res ? epi4_res_f8(ac, al + 4 * g4, be + 4 * g4, rg[g4], a.s_res, 0.f)
+                     : epi4_f8(ac, al + 4 * g4, be + 4 * g4, 0.f);
+      }
+      return mfma_to_store16(qv[0], qv[1], qv[2], qv[3]);
+    }
     unsigned rg[4] = {0, 0, 0, 0};
     if (res) {  // store layout -> MFMA layout
       unsigned rr[4] = {(unsigned)rs[0], (unsigned)rs[1], (unsigned)rs[2], (unsigned)rs[3]};
@@ -327,7 +379,7 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
             if (sm >= NR) sm -= NR;
             wa[t] = OFF_MID + (2 * h + lh) * PL + sm * PROW + 16 * (col + 1);
           }
-          v16i acc[2];
+          Acc acc[2];
           BT(0);
           run_job(ra[0], ra[1], acc);
           BT(1);
@@ -376,7 +428,7 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
             rq[t] = gload16_untracked(a.x + pix * LC + h * 32 + lh * 16);
           dst[t] = valid ? a.y + pix * LC + h * 32 + lh * 16 : g_trash_b + lane * 16;
         }
-        v16i acc[2];
+        Acc acc[2];
         BT(0);
         run_job(ra[0], ra[1], acc);
         BT(1);
@@ -416,7 +468,7 @@ bool block_l1_shape(int C, int OC, int H, int W) { return C == LC && OC == LC &&
 
 hipError_t launch_block_l1(const int8_t* x, int N, const int8_t* w1, const float* a1, const float* b1,
                            const int8_t* w2, const float* a2, const float* b2, float s_res, int8_t* y,
-                           hipStream_t s) {
+                           hipStream_t s, bool f8) {
   if (N <= 0) return hipSuccess;
   BlockArgs a{x, y, w1, w2, a1, b1, a2, b2, s_res, N};
   int grid = num_cus_b();
@@ -424,7 +476,10 @@ hipError_t launch_block_l1(const int8_t* x, int N, const int8_t* w1, const float
     const int g = std::atoi(e);
     if (g > 0 && g < grid) grid = g;
   }
-  hipLaunchKernelGGL(block_l1_kernel, dim3(N < grid ? N : grid), dim3(512), 0, s, a);
+  if (f8)
+    hipLaunchKernelGGL(block_l1_kernel<true>, dim3(N < grid ? N : grid), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL(block_l1_kernel<false>, dim3(N < grid ? N : grid), dim3(512), 0, s, a);
   return hipGetLastError();
 }
 

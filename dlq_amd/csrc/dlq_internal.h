@@ -62,7 +62,7 @@ hipError_t launch_conv3x3s2i(const ConvArgs& a, const int8_t* w_ds, const float*
 bool block_l1_shape(int C, int OC, int H, int W);
 hipError_t launch_block_l1(const int8_t* x, int N, const int8_t* w1, const float* a1, const float* b1,
                            const int8_t* w2, const float* a2, const float* b2, float s_res, int8_t* y,
-                           hipStream_t s);
+                           hipStream_t s, bool f8 = false);
 // Fused stem (stem.hip): quantise + conv1 7x7/s2 + BN/ReLU/requant + maxpool.
 size_t stem_packed_bytes();
 void pack_stem_weights(const int8_t* q_oihw, const float* alpha, int8_t* out, float* alpha_abs);

@@ -316,6 +316,18 @@ int dlq_stem_fused_f8(const float* x, int N, const uint8_t* w_stem, const float*
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("stem_fused_f8 launch: ") + hipGetErrorString(e));
 }
 
+int dlq_block_l1_nhwc_f8(const uint8_t* x, int N, const uint8_t* w1, const float* alpha1, const float* beta1,
+                         const uint8_t* w2, const float* alpha2, const float* beta2, float s_res, uint8_t* y,
+                         void* stream) {
+  if (N < 0) return fail(DLQ_ERR_ARG, "block_l1_f8: bad batch");
+  if (N == 0) return DLQ_OK;
+  if (!x || !w1 || !alpha1 || !beta1 || !w2 || !alpha2 || !beta2 || !y)
+    return fail(DLQ_ERR_ARG, "block_l1_f8: null pointer");
+  const hipError_t e = launch_block_l1((const int8_t*)x, N, (const int8_t*)w1, alpha1, beta1, (const int8_t*)w2, alpha2,
+                                       beta2, s_res, (int8_t*)y, (hipStream_t)stream, true);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("block_l1_f8 launch: ") + hipGetErrorString(e));
+}
+
 int dlq_gap_nhwc_f8(const uint8_t* x, int N, int C, int HW, float k, uint8_t* y, void* stream) {
   if (N < 0 || C <= 0 || C % 4 || HW <= 0) return fail(DLQ_ERR_ARG, "gap_f8: bad shape (C % 4 == 0)");
   if (N == 0) return DLQ_OK;

@@ -844,6 +844,18 @@ int forward_pass_f8(dlq_resnet18* m, const float* x, int B, float* logits, hipSt
     const ConvLayer& c1 = m->convs[b.c1];
     const ConvLayer& c2 = m->convs[b.c2];
     int8_t *h = m->buf[fi[0]], *dsb = m->buf[fi[1]], *out = m->buf[fi[2]];
+    if (fused_l1_block(m, b, H, H)) {  // both convs, the identity add and the ReLUs in one launch
+      if ((rc = mark(m, s, DLQ_FAM_L1))) return rc;
+      const float r_s = dlq::res_scale(m->scales.at(c1.in_site), m->scales.at(c2.site));
+      rc = dlq_block_l1_nhwc_f8((const uint8_t*)cur, B, (const uint8_t*)c1.w, c1.alpha, c1.beta, (const uint8_t*)c2.w,
+                                c2.alpha, c2.beta, r_s, (uint8_t*)out, s);
+      if (rc) return rc;
+      ci = fi[2];
+      cur = out;
+      if (record && b.name.size() == 8 && b.name[7] == '1')
+        if ((rc = record_stage(m, b.name.substr(0, 6).c_str(), cur, nB * H * H * b.oc, s))) return rc;
+      continue;
+    }
     if ((rc = conv_f8(m, c1, cur, B, H, nullptr, 0.f, true, h, s))) return rc;
     const int8_t* skip = cur;
     float s_skip = m->scales.at(c1.in_site);
@@ -1024,8 +1036,21 @@ int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes)
     auto fam = [&](const ConvLayer& c) {
       return f8_wide(c.Cstore, c.OC, c.H, c.H, c.k, c.k, c.s, c.s, c.p, c.p) ? DLQ_FAM_WIDE : DLQ_FAM_F8;
     };
+    for (const Block& b : m->blocks) {  // fused layer1 blocks: block input + output bytes
+      if (!fused_l1_block(m, b, m->convs[b.c1].H, m->convs[b.c1].H)) continue;
+      const ConvLayer& c1 = m->convs[b.c1];
+      macs[DLQ_FAM_L1] += 2.0 * c1.OC * c1.IC * 9 * c1.H * c1.H;
+      bytes[DLQ_FAM_L1] += 2.0 * c1.H * c1.H * c1.OC;
+    }
+    auto in_l1 = [&](const ConvLayer& c) {
+      for (const Block& b : m->blocks)
+        if ((&c == &m->convs[b.c1] || &c == &m->convs[b.c2]) && fused_l1_block(m, b, m->convs[b.c1].H, m->convs[b.c1].H))
+          return true;
+      return false;
+    };
     for (const ConvLayer& c : m->convs) {
       const int OH = out_dim(c.H, c.k, c.s, c.p);
+      if (in_l1(c)) continue;
       if (&c == &m->convs[m->stem] && !unfused_stem()) {  // fp32 input read + pooled e4m3 output
         macs[DLQ_FAM_STEM] = (double)c.OC * c.IC * c.k * c.k * OH * OH;
         bytes[DLQ_FAM_STEM] = 3.0 * 224 * 224 * 4 + 56.0 * 56 * 64;
@@ -1036,7 +1061,7 @@ int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes)
     }
     for (const Block& b : m->blocks) {  // conv2's residual read
       const ConvLayer& c2 = m->convs[b.c2];
-      bytes[fam(c2)] += (double)c2.H * c2.H * c2.OC;
+      if (!in_l1(c2)) bytes[fam(c2)] += (double)c2.H * c2.H * c2.OC;
     }
     macs[DLQ_FAM_FC] = 512.0 * 1000;
     bytes[DLQ_FAM_FC] = 512.0 + 4000.0;

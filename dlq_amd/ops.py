@@ -381,3 +381,15 @@ def stem_fused_f8(x: torch.Tensor, w_stem: torch.Tensor, alpha: torch.Tensor, be
     check(lib.dlq_stem_fused_f8(ptr(x), N, ptr(w_stem), ptr(alpha), ptr(beta), inv, ptr(y), stream_handle()),
           "stem_fused_f8")
     return y
+
+
+def block_l1_f8(x: torch.Tensor, w1: torch.Tensor, alpha1: torch.Tensor, beta1: torch.Tensor,
+                w2: torch.Tensor, alpha2: torch.Tensor, beta2: torch.Tensor, res_scale: float) -> torch.Tensor:
+    """e4m3 layer1 basic block in one launch: NHWC [N,56,56,64] -> same."""
+    _dev(x, torch.uint8)
+    if tuple(x.shape[1:]) != (56, 56, 64):
+        raise ValueError(f"block_l1 input must be [N,56,56,64], got {tuple(x.shape)}")
+    y = torch.empty_like(x)
+    check(lib.dlq_block_l1_nhwc_f8(ptr(x), x.shape[0], ptr(w1), ptr(alpha1), ptr(beta1), ptr(w2), ptr(alpha2),
+                                   ptr(beta2), float(res_scale), ptr(y), stream_handle()), "block_l1_f8")
+    return y

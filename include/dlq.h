@@ -404,6 +404,12 @@ int dlq_conv2d_nhwc_f8_acc(const dlq_conv_desc* d, const uint8_t* x, const uint8
 int dlq_pack_stem_weights_f8(const uint8_t* q_oihw, const float* alpha, uint8_t* packed, float* alpha_packed);
 int dlq_stem_fused_f8(const float* x, int N, const uint8_t* w_stem, const float* alpha, const float* beta,
                       float inv_s, uint8_t* y, void* stream);
+/* twin of dlq_block_l1_nhwc_s8 (the layer1 basic block in one launch;
+ * w1, w2 from dlq_pack_conv_weights_f8 for {N, 56, 56, 64, 64, 3, 3, 1, 1,
+ * 1, 1}).  Equal, within the conv bound, to two dlq_conv2d_nhwc_f8 calls. */
+int dlq_block_l1_nhwc_f8(const uint8_t* x, int N, const uint8_t* w1, const float* alpha1, const float* beta1,
+                         const uint8_t* w2, const float* alpha2, const float* beta2, float s_res, uint8_t* y,
+                         void* stream);
 /* twin of dlq_gap_nhwc_s8: exact sum of the values in units of 2^-9, then
  * requant(float(sum) * k) with k = s_in/HW/s_out * 2^-9.  The int8
  * dlq_maxpool2d_3x3_s2p1_nhwc_s8 applies unchanged to non-negative e4m3. */

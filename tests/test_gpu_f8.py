@@ -183,6 +183,34 @@ def test_stem_fused_f8_within_bound(gpu, N):
     _check_conv(got, ref, err, 3e-3, "stem")
 
 
+@pytest.mark.parametrize("N,grid", [(3, None), (5, "2")])
+def test_block_l1_f8_equals_two_convs(gpu, N, grid, monkeypatch):
+    """The fused layer1 block groups each tap's 64 channels into one MFMA in
+    the same lane order and tap order as the generic conv kernel, so it is
+    bit-identical to two dlq_conv2d_nhwc_f8 calls (which the oracle checks);
+    grid "2" puts several images in one workgroup (the DLQ_L1_GRID knob)."""
+    from dlq_amd import ops
+    if grid:
+        monkeypatch.setenv("DLQ_L1_GRID", grid)
+    rng = np.random.default_rng(53 + N)
+    x = O.quantize_f32_f8(np.abs(rng.standard_normal((N, 56, 56, 64))).astype(np.float32) * 30, 1.0)
+    ws, al, be = [], [], []
+    for _ in range(2):
+        w, bn = rand_conv(rng, 64, 64, 3)
+        wq, sw = O.quantize_weights_f8(w)
+        a_, b_ = O.fold_bn(0.02, sw, bn, 0.021)
+        ws.append(_cuda(ops.pack_conv_weights_f8(wq, 64, 56, 1, 1)))
+        al.append(_cuda(a_))
+        be.append(_cuda(b_))
+    r_s = float(O.res_scale(0.02, 0.021))
+    xd = _cuda(x)
+    y = ops.block_l1_f8(xd, ws[0], al[0], be[0], ws[1], al[1], be[1], r_s).cpu().numpy()
+    h = ops.conv2d_nhwc_f8(xd, ws[0], 64, 3, 1, 1, al[0], be[0], relu=True)
+    y2 = ops.conv2d_nhwc_f8(h, ws[1], 64, 3, 1, 1, al[1], be[1], residual=xd, res_scale=r_s, relu=True).cpu().numpy()
+    assert len(np.unique(y2)) > 50
+    assert np.array_equal(y, y2), f"{np.count_nonzero(y != y2)} of {y.size} codes differ"
+
+
 def test_gap_and_fc_f8_bitexact(gpu):
     from dlq_amd import ops
     rng = np.random.default_rng(23)
