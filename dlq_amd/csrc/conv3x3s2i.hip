@@ -25,6 +25,14 @@
 // weights [128][32 + 16] + patch; 2-slot LDS-DMA ring, the next stage issued
 // between the MFMAs right after the barrier that opens a stage.  Epilogues as
 // in conv3x3w.hip (permlane32 swaps into 16-byte stores).
+//
+// F8: e4m3 operands (the fp8 path), the same staged bytes and
+// LDS layout: each v_mfma_f32_32x32x64_f8f6f4 takes two taps of the 32-channel
+// slice (tap 8 paired with zeros, 5 MFMAs per slice); the downsample's MFMA
+// takes the pair (tap 4, tap 5) with its A fragment's upper half zero, so only
+// the centre tap contributes.  B pairs stream through a 3-deep register ring.
+#include <type_traits>
+
 #include "device_common.h"
 
 namespace dlq {
@@ -62,7 +70,7 @@ struct JGeo {
   static_assert((2 * WI + OW) * 16 < 65536, "tap offsets fit the ds_read immediate");
 };
 
-template <int OW, int C, int OUT, bool DS, int NF>
+template <int OW, int C, int OUT, bool DS, int NF, bool F8>
 __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, int8_t* y_ds, int8_t* lds,
                                          int mt, int f0) {
   using G = JGeo<OW, DS>;
@@ -158,7 +166,8 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     mid_off[f] = G::OFF_P + lh * G::UP * 16 + bu * 16;
     left_off[f] = ow == 0 ? G::OFF_Z + ((bu + OW - 1) & 15) * 16 : mid_off[f] + (OW - 1) * 16;
   }
-  v16i acc[NF], accd[DS ? NF : 1];
+  using Acc = typename std::conditional<F8, v16f, v16i>::type;
+  Acc acc[NF], accd[DS ? NF : 1];
   int cur_ot = 0, cur_p0 = 0;
 
   prep_for(0);
@@ -178,8 +187,8 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
       item_of(li, cur_ot, cur_p0);
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
-        acc[f] = v16i{0};
-        if constexpr (DS) accd[f] = v16i{0};
+        acc[f] = Acc{0};
+        if constexpr (DS) accd[f] = Acc{0};
       }
     }
     const int sb = (s & 1) * G::SLOT;
@@ -192,6 +201,51 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
       }
     }
     const int8_t* abase = lds + sb + a_row;
+    if constexpr (F8) {
+      constexpr int NPAIR = 5, NM = NPAIR * NF, D = 3;
+      auto ld_half = [&](int tap, int f) -> v4i {
+        const int kh = tap / 3, kw = tap % 3;
+        const int base = kw == 0 ? left_off[f] : mid_off[f];
+        return *(const v4i*)(lds + base + (kh * G::WI + (kw == 2 ? OW : 0)) * 16);
+      };
+      auto ld_a2 = [&](int pr) -> v8i {
+        const v4i lo = *(const v4i*)(abase + (2 * pr) * 32);
+        const v4i hi = 2 * pr + 1 < 9 ? *(const v4i*)(abase + (2 * pr + 1) * 32) : v4i{0, 0, 0, 0};
+        return cat8(lo, hi);
+      };
+      auto ld_b2 = [&](int i) -> v8i {
+        const int pr = i / NF, f = i - pr * NF;
+        const v4i lo = ld_half(2 * pr, f);
+        const v4i hi = 2 * pr + 1 < 9 ? ld_half(2 * pr + 1, f) : v4i{0, 0, 0, 0};
+        return cat8(lo, hi);
+      };
+      v8i fa2[2], fbr[D], fd2;
+      fa2[0] = ld_a2(0);
+#pragma unroll
+      for (int i = 0; i < D; ++i) fbr[i] = ld_b2(i);
+#pragma unroll
+      for (int pr = 0; pr < NPAIR; ++pr) {
+        if (pr + 1 < NPAIR) fa2[(pr + 1) & 1] = ld_a2(pr + 1);
+        if constexpr (DS) {
+          if (pr == 1) fd2 = cat8(*(const v4i*)(lds + sb + d_row), v4i{0, 0, 0, 0});  // used with pair (4, 5)
+        }
+        const int k0 = 2 * pr * DPW / 9, k1 = (2 * pr + 2 < 9 ? 2 * pr + 2 : 9) * DPW / 9;
+        if (more && !(a.dbg & 2)) {
+#pragma unroll
+          for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          const int i = pr * NF + f;
+          acc[f] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa2[pr & 1], fbr[i % D], acc[f], 0, 0, 0, 0, 0, 0);
+          if constexpr (DS) {
+            if (pr == 2)
+              accd[f] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fd2, fbr[i % D], accd[f], 0, 0, 0, 0, 0, 0);
+          }
+          if (i + D < NM) fbr[i % D] = ld_b2(i + D);
+        }
+      }
+    } else {
     v4i fa[2], fb[NF], fd;
     auto ld_b = [&](int tap, int f) {
       const int kh = tap / 3, kw = tap % 3;
@@ -243,6 +297,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
         __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
       }
     }
+    }  // int8 MFMA loop
 
     if (j != NS - 1) continue;
     // ---- fused epilogues of the item ----
@@ -255,11 +310,15 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
         for (int g = 0; g < 4; ++g) {
           const int oc = cur_ot * JOT + mt * 32 + 8 * g + 4 * lh;
           v4i* dst = keep ? (v4i*)((int*)a.y + (size_t)p * a.OC + oc) : (v4i*)(g_trash_s2i + lane * 16);
-          *dst = v4i{acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
+          if constexpr (F8)  // raw fp32 accumulators
+            *dst = v4i{__float_as_int(acc[f][4 * g]), __float_as_int(acc[f][4 * g + 1]),
+                       __float_as_int(acc[f][4 * g + 2]), __float_as_int(acc[f][4 * g + 3])};
+          else
+            *dst = v4i{acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
         }
       }
     } else {
-      auto epi = [&](const v16i* ac, int ab_off, float lo, int8_t* out) {
+      auto epi = [&](const Acc* ac, int ab_off, float lo, int8_t* out) {
         float al[4][4], be[4][4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -277,8 +336,13 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
           unsigned q[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const int a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
-            q[g] = epi4(a4, al[g], be[g], lo);
+            if constexpr (F8) {
+              const float a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
+              q[g] = epi4_f8(a4, al[g], be[g], lo);
+            } else {
+              const int a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
+              q[g] = epi4(a4, al[g], be[g], lo);
+            }
           }
           swap32(q[0], q[2]);
           swap32(q[1], q[3]);
@@ -289,15 +353,16 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
           *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
         }
       };
-      epi(acc, 0, a.relu ? 0.f : -127.f, (int8_t*)a.y);
-      if constexpr (DS) epi(accd, 2 * OC * 4, -127.f, y_ds);
+      constexpr float LO = F8 ? -448.f : -127.f;
+      epi(acc, 0, a.relu ? 0.f : LO, (int8_t*)a.y);
+      if constexpr (DS) epi(accd, 2 * OC * 4, LO, y_ds);
     }
   }
   wait_vm0();
 }
 
 // OUT: 0 = int8 (fused epilogues), 2 = int32 conv1 accumulators (DS = false).
-template <int OW, int C, int OUT, bool DS>
+template <int OW, int C, int OUT, bool DS, bool F8>
 __global__ __launch_bounds__(JNW * 64, 1) void conv3x3s2i_kernel(ConvArgs a, const int8_t* w_ds, const float* al_ds,
                                                                  const float* be_ds, int8_t* y_ds) {
   using G = JGeo<OW, DS>;
@@ -324,9 +389,9 @@ __global__ __launch_bounds__(JNW * 64, 1) void conv3x3s2i_kernel(ConvArgs a, con
   __syncthreads();
   const int wave = tid >> 6;
   if (wave < 4)
-    s2i_body<OW, C, OUT, DS, 4>(a, w_ds, y_ds, lds, wave & 3, 0);
+    s2i_body<OW, C, OUT, DS, 4, F8>(a, w_ds, y_ds, lds, wave & 3, 0);
   else
-    s2i_body<OW, C, OUT, DS, 3>(a, w_ds, y_ds, lds, wave & 3, 4);
+    s2i_body<OW, C, OUT, DS, 3, F8>(a, w_ds, y_ds, lds, wave & 3, 4);
 }
 
 int num_cus_s2i() {
@@ -340,22 +405,34 @@ int num_cus_s2i() {
   return n;
 }
 
-template <int OW, int C>
+template <int OW, int C, bool F8>
 hipError_t launch_j(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, const float* be_ds,
                     int8_t* y_ds, hipStream_t s) {
   const int NI = (a.OCp / JOT) * ((a.P + JL - 1) / JL), ncu = num_cus_s2i();
   const dim3 grid(NI < ncu ? NI : ncu), block(JNW * 64);
   if (a.out_kind == 2) {
     if (w_ds) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 2, false>), grid, block, 0, s, a, nullptr, nullptr, nullptr,
+    hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 2, false, F8>), grid, block, 0, s, a, nullptr, nullptr, nullptr,
                        nullptr);
   } else if (w_ds) {
-    hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true>), grid, block, 0, s, a, w_ds, al_ds, be_ds, y_ds);
+    hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true, F8>), grid, block, 0, s, a, w_ds, al_ds, be_ds, y_ds);
   } else {
-    hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, false>), grid, block, 0, s, a, nullptr, nullptr, nullptr,
+    hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, false, F8>), grid, block, 0, s, a, nullptr, nullptr, nullptr,
                        nullptr);
   }
   return hipGetLastError();
+}
+
+template <bool F8>
+hipError_t launch_s2i(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, const float* be_ds, int8_t* y_ds,
+                      hipStream_t s) {
+  if (a.OCp != a.OC || a.OC != 2 * a.C || a.H != a.W || a.OW * 2 != a.W) return hipErrorInvalidValue;
+  switch (a.W) {
+    case 56: return a.C == 64 ? launch_j<28, 64, F8>(a, w_ds, al_ds, be_ds, y_ds, s) : hipErrorInvalidValue;
+    case 28: return a.C == 128 ? launch_j<14, 128, F8>(a, w_ds, al_ds, be_ds, y_ds, s) : hipErrorInvalidValue;
+    case 14: return a.C == 256 ? launch_j<7, 256, F8>(a, w_ds, al_ds, be_ds, y_ds, s) : hipErrorInvalidValue;
+  }
+  return hipErrorInvalidValue;
 }
 
 }  // namespace
@@ -364,13 +441,13 @@ hipError_t launch_j(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, c
 // conv1, downsample_pack for the 1x1).
 hipError_t launch_conv3x3s2i(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, const float* be_ds,
                              int8_t* y_ds, hipStream_t s) {
-  if (a.OCp != a.OC || a.OC != 2 * a.C || a.H != a.W || a.OW * 2 != a.W) return hipErrorInvalidValue;
-  switch (a.W) {
-    case 56: return a.C == 64 ? launch_j<28, 64>(a, w_ds, al_ds, be_ds, y_ds, s) : hipErrorInvalidValue;
-    case 28: return a.C == 128 ? launch_j<14, 128>(a, w_ds, al_ds, be_ds, y_ds, s) : hipErrorInvalidValue;
-    case 14: return a.C == 256 ? launch_j<7, 256>(a, w_ds, al_ds, be_ds, y_ds, s) : hipErrorInvalidValue;
-  }
-  return hipErrorInvalidValue;
+  return launch_s2i<false>(a, w_ds, al_ds, be_ds, y_ds, s);
+}
+
+// e4m3 operands; the same weight images (conv3x3w_pack / downsample_pack of the codes).
+hipError_t launch_conv3x3s2i_f8(const ConvArgs& a, const uint8_t* w_ds, const float* al_ds, const float* be_ds,
+                                uint8_t* y_ds, hipStream_t s) {
+  return launch_s2i<true>(a, (const int8_t*)w_ds, al_ds, be_ds, (int8_t*)y_ds, s);
 }
 
 }  // namespace dlq

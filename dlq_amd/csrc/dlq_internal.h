@@ -86,7 +86,11 @@ hipError_t launch_im2col_nchw(const int8_t* x, int N, int C, int H, int W, int k
 hipError_t launch_conv_f8(const ConvArgs& a, hipStream_t s);
 // conv3x3i with e4m3 operands (wide stride-1 shapes, conv3x3w_pack image).
 hipError_t launch_conv3x3i_f8(const ConvArgs& a, hipStream_t s);
-// fp8 weight image choice: the wide layout for conv3x3w_shape, else generic.
+// conv3x3s2i with e4m3 operands (+ the fused 1x1/s2 downsample when w_ds).
+hipError_t launch_conv3x3s2i_f8(const ConvArgs& a, const uint8_t* w_ds, const float* alpha_ds, const float* beta_ds,
+                                uint8_t* y_ds, hipStream_t s);
+// fp8 weight image choice: the wide layout for conv3x3w_shape and
+// conv3x3s2_shape, else generic.
 bool f8_wide(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW);
 size_t packed_bytes_f8(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW);
 void pack_conv_weights_f8(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW,

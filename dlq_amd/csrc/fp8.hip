@@ -146,6 +146,107 @@ __global__ __launch_bounds__(256) void linear_f8_kernel(const uint8_t* __restric
     if (n0 + r < N) y[(size_t)(n0 + r) * O + o] = __builtin_fmaf((float)acc[r], alpha[o], beta[o]);
 }
 
+// GAP for C % 16 == 0 (the network's shape): head.hip's gap16 structure --
+// one thread = 16 channels x an eighth of the pixels, two 16-byte loads in
+// flight, three xor-shuffles -- on exact integer unit sums (the same sums as
+// gap_f8_kernel, so the same result).
+__device__ __forceinline__ void add_units16(int* s, const v4i v) {
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    s[4 * w + 0] += f8_units(v[w], 0);
+    s[4 * w + 1] += f8_units(v[w], 1);
+    s[4 * w + 2] += f8_units(v[w], 2);
+    s[4 * w + 3] += f8_units(v[w], 3);
+  }
+}
+
+__global__ __launch_bounds__(256) void gap16_f8_kernel(const uint8_t* __restrict__ x, int N, int C, int HW, float k,
+                                                       uint8_t* __restrict__ y) {
+  const int tpi = (C / 16) * 8;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = (int)(t / tpi), r = (int)(t - (long)n * tpi);
+  const int pg = r & 7, cg = r >> 3;
+  int s[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s[i] = 0;
+  if (n < N) {
+    const uint8_t* src = x + (size_t)n * HW * C + cg * 16;
+    int i = pg;
+    for (; i + 8 < HW; i += 16) {
+      const v4i v0 = *(const v4i*)(src + (size_t)i * C);
+      const v4i v1 = *(const v4i*)(src + (size_t)(i + 8) * C);
+      add_units16(s, v0);
+      add_units16(s, v1);
+    }
+    if (i < HW) add_units16(s, *(const v4i*)(src + (size_t)i * C));
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    s[i] += __shfl_xor(s[i], 1);
+    s[i] += __shfl_xor(s[i], 2);
+    s[i] += __shfl_xor(s[i], 4);
+  }
+  if (n < N && pg == 0) {
+    v4i o;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+      o[w] = (int)enc4_f8((float)s[4 * w] * k, (float)s[4 * w + 1] * k, (float)s[4 * w + 2] * k,
+                          (float)s[4 * w + 3] * k, -448.f);
+    *(v4i*)(y + (size_t)n * C + cg * 16) = o;
+  }
+}
+
+// FC for K % 64 == 0 on v_mfma_f64_16x16x4f64: the e4m3 codes are decoded to
+// fp64 (exact) and every partial sum is a multiple of 2^-18 below 2^35, so
+// the f64 MFMA's sums are exact in any order -- the same acc as
+// linear_f8_kernel.  One wave = 16 rows n x 16 outputs o; each lane streams
+// 16-byte pieces of one x row and one w row, and MFMA s of a 64-deep chunk
+// takes byte s of every lane's 16-byte piece (the same k for A and B).
+// Block = 4 waves = 16 rows x 64 outputs.
+__global__ __launch_bounds__(256) void linear_f8_mfma_kernel(const uint8_t* __restrict__ x, int N, int K,
+                                                             const uint8_t* __restrict__ w, int O,
+                                                             const float* __restrict__ alpha,
+                                                             const float* __restrict__ beta, float* __restrict__ y) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.y * 16, o0 = blockIdx.x * 64 + wave * 16;
+  const int n = min(n0 + li, N - 1), o = min(o0 + li, O - 1);
+  const uint8_t* xr = x + (size_t)n * K + g * 16;
+  const uint8_t* wr = w + (size_t)o * K + g * 16;
+  typedef double v4d __attribute__((ext_vector_type(4)));
+  v4d acc = {0.0, 0.0, 0.0, 0.0};
+  auto dec = [](int word, int sel) -> double {
+    float v;
+    switch (sel) {
+      case 0: v = __builtin_amdgcn_cvt_f32_fp8(word, 0); break;
+      case 1: v = __builtin_amdgcn_cvt_f32_fp8(word, 1); break;
+      case 2: v = __builtin_amdgcn_cvt_f32_fp8(word, 2); break;
+      default: v = __builtin_amdgcn_cvt_f32_fp8(word, 3); break;
+    }
+    return (double)v;
+  };
+  v4i xa = *(const v4i*)xr, wb = *(const v4i*)wr;
+  for (int k0 = 0; k0 < K; k0 += 64) {
+    const v4i xc = xa, wc = wb;
+    if (k0 + 64 < K) {  // next chunk's pieces in flight during this chunk's MFMAs
+      xa = *(const v4i*)(xr + k0 + 64);
+      wb = *(const v4i*)(wr + k0 + 64);
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(dec(xc[s >> 2], s & 3), dec(wc[s >> 2], s & 3), acc, 0, 0, 0);
+  }
+  // D[i][j] (f64 layout, cdna_hip_programming.md): row i = n (g + 4 * e), column j = o (li)
+  const int oc = o0 + li;
+  if (oc >= O) return;
+  const float al = alpha[oc], be = beta[oc];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int nr = n0 + g + 4 * e;
+    if (nr < N) y[(size_t)nr * O + oc] = __builtin_fmaf((float)acc[e], al, be);
+  }
+}
+
 int grid_for(long total) {
   long g = (total + 255) / 256;
   if (g > 256 * 32) g = 256 * 32;
@@ -191,8 +292,15 @@ uint8_t f8_requant_host(float y, float lo) {
 // on the generic kernel and layout.
 bool f8_wide(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW) {
   const char* e = std::getenv("DLQ_F8_GENERIC");
-  return !(e && e[0] == '1') && conv3x3w_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW);
+  return !(e && e[0] == '1') && (conv3x3w_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW) ||
+                                 conv3x3s2_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW));
 }
+
+namespace {
+hipError_t launch_wide_f8(const ConvArgs& a, hipStream_t s) {
+  return a.sH == 2 ? launch_conv3x3s2i_f8(a, nullptr, nullptr, nullptr, nullptr, s) : launch_conv3x3i_f8(a, s);
+}
+}  // namespace
 
 size_t packed_bytes_f8(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW) {
   if (f8_wide(C, OC, H, W, kH, kW, sH, sW, pH, pW)) return conv3x3w_packed_bytes(OC, C);
@@ -280,9 +388,27 @@ int dlq_conv2d_nhwc_f8(const dlq_conv_desc* d, const uint8_t* x, const uint8_t* 
                              res_scale, relu, DLQ_OUT_S8, y, a);
   if (rc) return rc;
   if (a.P == 0) return DLQ_OK;
-  const hipError_t e = f8_wide(F8_GEOM(d)) ? launch_conv3x3i_f8(a, (hipStream_t)stream)
+  const hipError_t e = f8_wide(F8_GEOM(d)) ? launch_wide_f8(a, (hipStream_t)stream)
                                            : launch_conv_f8(a, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d_f8 launch: ") + hipGetErrorString(e));
+}
+
+int dlq_conv2d_s2_ds_nhwc_f8(const dlq_conv_desc* d, const uint8_t* x, const uint8_t* w_packed, const float* alpha,
+                             const float* beta, const uint8_t* w_ds, const float* alpha_ds, const float* beta_ds,
+                             uint8_t* y, uint8_t* y_ds, void* stream) {
+  if (!d || !conv3x3s2_shape(F8_GEOM(d)))
+    return fail(DLQ_ERR_ARG, "conv2d_s2_ds_f8: needs a 3x3/s2/p1 C->2C conv at 56x56x64, 28x28x128 or 14x14x256");
+  if (!alpha || !beta || !w_ds || !alpha_ds || !beta_ds || !y_ds)
+    return fail(DLQ_ERR_ARG, "conv2d_s2_ds_f8: null pointer");
+  if (!f8_wide(F8_GEOM(d))) return fail(DLQ_ERR_STATE, "conv2d_s2_ds_f8: disabled by DLQ_F8_GENERIC");
+  ConvArgs a;
+  int rc = conv_args_checked(d, (const int8_t*)x, (const int8_t*)w_packed, alpha, beta, nullptr, 0.f, 1, DLQ_OUT_S8,
+                             y, a);
+  if (rc) return rc;
+  if (a.P == 0) return DLQ_OK;
+  const hipError_t e = launch_conv3x3s2i_f8(a, w_ds, alpha_ds, beta_ds, y_ds, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK
+                         : fail(DLQ_ERR_LAUNCH, std::string("conv2d_s2_ds_f8 launch: ") + hipGetErrorString(e));
 }
 
 int dlq_conv2d_nhwc_f8_acc(const dlq_conv_desc* d, const uint8_t* x, const uint8_t* w_packed, float* acc,
@@ -294,7 +420,7 @@ int dlq_conv2d_nhwc_f8_acc(const dlq_conv_desc* d, const uint8_t* x, const uint8
                              DLQ_OUT_S32, acc, a);
   if (rc) return rc;
   if (a.P == 0) return DLQ_OK;
-  const hipError_t e = f8_wide(F8_GEOM(d)) ? launch_conv3x3i_f8(a, (hipStream_t)stream)
+  const hipError_t e = f8_wide(F8_GEOM(d)) ? launch_wide_f8(a, (hipStream_t)stream)
                                            : launch_conv_f8(a, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d_f8_acc launch: ") + hipGetErrorString(e));
 }
@@ -333,8 +459,14 @@ int dlq_gap_nhwc_f8(const uint8_t* x, int N, int C, int HW, float k, uint8_t* y,
   if (N == 0) return DLQ_OK;
   if (!x || !y) return fail(DLQ_ERR_ARG, "gap_f8: null pointer");
   if ((long long)HW * 229376 >= (1LL << 31)) return fail(DLQ_ERR_ARG, "gap_f8: HW too large for exact int32 sums");
-  hipLaunchKernelGGL(gap_f8_kernel, dim3(grid_for((long)N * (C / 4))), dim3(256), 0, (hipStream_t)stream, x, N, C,
-                     HW, k, y);
+  if (C % 16 == 0) {
+    const long total = (long)N * (C / 16) * 8;
+    hipLaunchKernelGGL(gap16_f8_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                       N, C, HW, k, y);
+  } else {
+    hipLaunchKernelGGL(gap_f8_kernel, dim3(grid_for((long)N * (C / 4))), dim3(256), 0, (hipStream_t)stream, x, N, C,
+                       HW, k, y);
+  }
   return launch_result("gap_f8");
 }
 
@@ -343,6 +475,11 @@ int dlq_linear_f8(const uint8_t* x, int N, int K, const uint8_t* w, int O, const
   if (N < 0 || K <= 0 || K % 4 || O <= 0) return fail(DLQ_ERR_ARG, "linear_f8: bad shape (K % 4 == 0)");
   if (N == 0) return DLQ_OK;
   if (!x || !w || !alpha || !beta || !y) return fail(DLQ_ERR_ARG, "linear_f8: null pointer");
+  if (K % 64 == 0 && !((uintptr_t)w & 15) && !((uintptr_t)x & 15)) {  // f64 MFMA kernel
+    const dim3 grid((O + 63) / 64, (N + 15) / 16);
+    hipLaunchKernelGGL(linear_f8_mfma_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, N, K, w, O, alpha, beta, y);
+    return launch_result("linear_f8");
+  }
   if ((size_t)kFcImgs * K * 4 > 64 * 1024) return fail(DLQ_ERR_ARG, "linear_f8: K too large");
   if ((uintptr_t)w & 3) return fail(DLQ_ERR_ARG, "linear_f8: misaligned weights");
   const dim3 grid((O + 255) / 256, (N + kFcImgs - 1) / kFcImgs);

@@ -621,6 +621,11 @@ int prepare_f8(dlq_resnet18* m, int max_batch) {
     if ((rc = upload(m, &c.w, packed.data(), packed.size())) || (rc = upload(m, &c.alpha, alpha.data(), ocp * 4)) ||
         (rc = upload(m, &c.beta, beta.data(), ocp * 4)))
       return rc;
+    if (c.k == 1 && c.s == 2 && c.Cstore % 32 == 0) {  // the downsample's image for the fused s2 launch
+      std::vector<int8_t> fp(downsample_packed_bytes(c.OC, c.Cstore));
+      downsample_pack((const int8_t*)q.data(), c.OC, c.IC, c.Cstore, fp.data());
+      if ((rc = upload(m, &c.wf, fp.data(), fp.size()))) return rc;
+    }
     if (&c == &m->convs[m->stem]) {  // the fused stem's image (sign bits of alpha < 0 rows flipped)
       std::vector<uint8_t> sp(stem_packed_bytes());
       std::vector<float> sa(64);
@@ -856,10 +861,21 @@ int forward_pass_f8(dlq_resnet18* m, const float* x, int B, float* logits, hipSt
         if ((rc = record_stage(m, b.name.substr(0, 6).c_str(), cur, nB * H * H * b.oc, s))) return rc;
       continue;
     }
-    if ((rc = conv_f8(m, c1, cur, B, H, nullptr, 0.f, true, h, s))) return rc;
     const int8_t* skip = cur;
     float s_skip = m->scales.at(c1.in_site);
-    if (b.down) {
+    if (b.down && m->convs[b.ds].wf && f8_wide(c1.Cstore, c1.OC, H, H, 3, 3, 2, 2, 1, 1)) {
+      // conv1 (3x3/s2) and the 1x1/s2 downsample in one launch
+      const ConvLayer& ds = m->convs[b.ds];
+      if ((rc = mark(m, s, DLQ_FAM_S2DS))) return rc;
+      dlq_conv_desc d{B, H, H, c1.Cstore, c1.OC, 3, 3, 2, 2, 1, 1};
+      rc = dlq_conv2d_s2_ds_nhwc_f8(&d, (const uint8_t*)cur, (const uint8_t*)c1.w, c1.alpha, c1.beta,
+                                    (const uint8_t*)ds.wf, ds.alpha, ds.beta, (uint8_t*)h, (uint8_t*)dsb, s);
+      if (rc) return rc;
+      skip = dsb;
+      s_skip = m->scales.at(ds.site);
+    } else if ((rc = conv_f8(m, c1, cur, B, H, nullptr, 0.f, true, h, s))) {
+      return rc;
+    } else if (b.down) {
       const ConvLayer& ds = m->convs[b.ds];
       if ((rc = conv_f8(m, ds, cur, B, H, nullptr, 0.f, false, dsb, s))) return rc;
       skip = dsb;
@@ -1032,7 +1048,7 @@ int dlq_resnet18_timing(dlq_resnet18* m, double* ms, int* launches, int* forward
 int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes) {
   if (!m || !macs || !bytes) return fail(DLQ_ERR_ARG, "family_work: null");
   for (int f = 0; f < DLQ_FAM_COUNT; ++f) macs[f] = bytes[f] = 0.0;
-  if (m->prec == DLQ_PREC_FP8) {  // one launch per conv: conv3x3i<F8> (wide) or conv_s8_kernel<F8>
+  if (m->prec == DLQ_PREC_FP8) {  // stem, layer1 blocks, s2 + downsample, conv3x3i<F8> (wide), GAP, FC
     auto fam = [&](const ConvLayer& c) {
       return f8_wide(c.Cstore, c.OC, c.H, c.H, c.k, c.k, c.s, c.s, c.p, c.p) ? DLQ_FAM_WIDE : DLQ_FAM_F8;
     };
@@ -1048,9 +1064,25 @@ int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes)
           return true;
       return false;
     };
+    // 0: not in a fused stride-2 launch, 1: its 3x3 conv1, 2: its downsample
+    auto in_s2ds = [&](const ConvLayer& c) {
+      for (const Block& b : m->blocks) {
+        if (!b.down || !m->convs[b.ds].wf) continue;
+        const ConvLayer& c1 = m->convs[b.c1];
+        if (!f8_wide(c1.Cstore, c1.OC, c1.H, c1.H, 3, 3, 2, 2, 1, 1)) continue;
+        if (&c == &c1) return 1;
+        if (&c == &m->convs[b.ds]) return 2;
+      }
+      return 0;
+    };
     for (const ConvLayer& c : m->convs) {
       const int OH = out_dim(c.H, c.k, c.s, c.p);
       if (in_l1(c)) continue;
+      if (const int k = in_s2ds(c)) {  // one launch: the shared input once, both outputs
+        macs[DLQ_FAM_S2DS] += (double)c.OC * c.IC * c.k * c.k * OH * OH;
+        bytes[DLQ_FAM_S2DS] += (k == 1 ? (double)c.H * c.H * c.Cstore : 0.0) + (double)OH * OH * c.OC;
+        continue;
+      }
       if (&c == &m->convs[m->stem] && !unfused_stem()) {  // fp32 input read + pooled e4m3 output
         macs[DLQ_FAM_STEM] = (double)c.OC * c.IC * c.k * c.k * OH * OH;
         bytes[DLQ_FAM_STEM] = 3.0 * 224 * 224 * 4 + 56.0 * 56 * 64;

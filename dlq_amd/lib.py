@@ -110,6 +110,7 @@ _SIGS = {
     "dlq_resnet18_set_precision": ([_vp, _i], _i),
     "dlq_pack_stem_weights_f8": ([_vp, _vp, _vp, _vp], _i),
     "dlq_stem_fused_f8": ([_vp, _i, _vp, _vp, _vp, _f, _vp, _vp], _i),
+    "dlq_conv2d_s2_ds_nhwc_f8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "dlq_block_l1_nhwc_f8": ([_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, C.c_float, _vp, _vp], _i),
 }
 

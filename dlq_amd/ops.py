@@ -383,6 +383,22 @@ def stem_fused_f8(x: torch.Tensor, w_stem: torch.Tensor, alpha: torch.Tensor, be
     return y
 
 
+def conv2d_s2_ds_nhwc_f8(x: torch.Tensor, w_packed: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor,
+                         w_ds: torch.Tensor, alpha_ds: torch.Tensor, beta_ds: torch.Tensor):
+    """e4m3 twin of conv2d_s2_ds_nhwc_s8 (w_ds = pack_downsample_weights of the
+    e4m3 codes viewed as int8): returns (y, y_ds), uint8 [N, H/2, W/2, 2C]."""
+    _dev(x, torch.uint8)
+    N, H, W, Cc = x.shape
+    OC = 2 * Cc
+    y = torch.empty((N, H // 2, W // 2, OC), dtype=torch.uint8, device=x.device)
+    y_ds = torch.empty_like(y)
+    d = ConvDesc(N, H, W, Cc, OC, 3, 3, 2, 2, 1, 1)
+    check(lib.dlq_conv2d_s2_ds_nhwc_f8(C.byref(d), ptr(x), ptr(w_packed), ptr(alpha), ptr(beta), ptr(w_ds),
+                                       ptr(alpha_ds), ptr(beta_ds), ptr(y), ptr(y_ds), stream_handle()),
+          "conv2d_s2_ds_nhwc_f8")
+    return y, y_ds
+
+
 def block_l1_f8(x: torch.Tensor, w1: torch.Tensor, alpha1: torch.Tensor, beta1: torch.Tensor,
                 w2: torch.Tensor, alpha2: torch.Tensor, beta2: torch.Tensor, res_scale: float) -> torch.Tensor:
     """e4m3 layer1 basic block in one launch: NHWC [N,56,56,64] -> same."""

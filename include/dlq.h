@@ -384,8 +384,9 @@ int dlq_quantize_f32_f8(const float* x, size_t n, float inv_s, uint8_t* q, void*
 /* twin of dlq_quantize_nchw_to_nhwc_s8. */
 int dlq_quantize_nchw_to_nhwc_f8(const float* x, int N, int C, int H, int W, int Cout, float inv_s, uint8_t* y,
                                  void* stream);
-/* Generic packed image (C % 64 == 0 or the 7x7 C == 4 stem; the wide int8
- * layouts are not used by the fp8 path). */
+/* Packed image: the int8 wide layout (dlq_pack_conv_weights_s8's) for the
+ * layer2-4 3x3 convs (stride 1 and the stride-2 conv1s), else the generic
+ * one (C % 64 == 0 or the 7x7 C == 4 stem). */
 size_t dlq_conv_packed_bytes_f8(const dlq_conv_desc* d);
 int dlq_pack_conv_weights_f8(const dlq_conv_desc* d, const uint8_t* q_oihw, int IC, uint8_t* packed);
 /* twin of dlq_conv2d_nhwc_s8 (DLQ_OUT_S8 semantics, e4m3 in and out):
@@ -393,6 +394,14 @@ int dlq_pack_conv_weights_f8(const dlq_conv_desc* d, const uint8_t* q_oihw, int 
 int dlq_conv2d_nhwc_f8(const dlq_conv_desc* d, const uint8_t* x, const uint8_t* w_packed, const float* alpha,
                        const float* beta, const uint8_t* residual, float res_scale, int relu, uint8_t* y,
                        void* stream);
+/* twin of dlq_conv2d_s2_ds_nhwc_s8: the 3x3/s2 conv (+BN+ReLU, w_packed from
+ * dlq_pack_conv_weights_f8) and the block's 1x1/s2 downsample (+BN, w_ds =
+ * dlq_pack_downsample_weights_s8 of the e4m3 codes: the packing moves bytes)
+ * of one input in one launch.  Each equals its dlq_conv2d_nhwc_f8 call within
+ * the conv bound. */
+int dlq_conv2d_s2_ds_nhwc_f8(const dlq_conv_desc* d, const uint8_t* x, const uint8_t* w_packed, const float* alpha,
+                             const float* beta, const uint8_t* w_ds, const float* alpha_ds, const float* beta_ds,
+                             uint8_t* y, uint8_t* y_ds, void* stream);
 /* The raw fp32 accumulators of the same conv (twin of DLQ_OUT_S32): acc
  * NHWC [N][OH][OW][OC] fp32 (parity / debugging). */
 int dlq_conv2d_nhwc_f8_acc(const dlq_conv_desc* d, const uint8_t* x, const uint8_t* w_packed, float* acc,

@@ -211,10 +211,47 @@ def test_block_l1_f8_equals_two_convs(gpu, N, grid, monkeypatch):
     assert np.array_equal(y, y2), f"{np.count_nonzero(y != y2)} of {y.size} codes differ"
 
 
-def test_gap_and_fc_f8_bitexact(gpu):
+@pytest.mark.parametrize("C,H,N", [(64, 56, 3), (128, 28, 5), (256, 14, 37)])
+def test_s2_conv_with_fused_downsample_f8(gpu, C, H, N):
+    """layerX.0 with e4m3 operands: 3x3/s2 conv1 (+BN+ReLU) and the 1x1/s2
+    downsample (+BN) from ONE launch.  Both outputs within the conv bound of
+    the oracle; conv1's equals the standalone dlq_conv2d_nhwc_f8 call (the
+    same kernel without the downsample) code for code."""
     from dlq_amd import ops
-    rng = np.random.default_rng(23)
-    x = O.quantize_f32_f8(np.abs(rng.standard_normal((5, 512, 7, 7))).astype(np.float32) * 30, 1.0)
+    rng = np.random.default_rng(C * 11 + N)
+    OC = 2 * C
+    x = O.quantize_f32_f8(np.abs(rng.standard_normal((N, C, H, H))).astype(np.float32) * 40, 1.0)
+    w, bn = rand_conv(rng, OC, C, 3)
+    wd, bnd = rand_conv(rng, OC, C, 1)
+    bnd[0][::5] *= -1
+    wq, sw = O.quantize_weights_f8(w)
+    wdq, swd = O.quantize_weights_f8(wd)
+    s_x, s_y, s_d = 0.011, 0.013, 0.015
+    alpha, beta = O.fold_bn(s_x, sw, bn, s_y)
+    alpha_d, beta_d = O.fold_bn(s_x, swd, bnd, s_d)
+    ref = O.epilogue_f8(O.conv_f8_acc(x, wq, 2, 1), alpha, beta, None, 0.0, True)
+    ref_d = O.epilogue_f8(O.conv_f8_acc(x, wdq, 2, 0), alpha_d, beta_d, None, 0.0, False)
+    xd = _cuda(nchw_to_nhwc(x))
+    wdev = _cuda(ops.pack_conv_weights_f8(wq, C, H, 2, 1))
+    wds = _cuda(ops.pack_downsample_weights(wdq.reshape(OC, C).view(np.int8), C))
+    y, y_ds = ops.conv2d_s2_ds_nhwc_f8(xd, wdev, _cuda(alpha), _cuda(beta), wds, _cuda(alpha_d), _cuda(beta_d))
+    got, got_d = nhwc_to_nchw(y.cpu().numpy()), nhwc_to_nchw(y_ds.cpu().numpy())
+    for g, r, wqq, al, s_, p_, what in ((got, ref, wq, alpha, 2, 1, "conv1"), (got_d, ref_d, wdq, alpha_d, 2, 0, "ds")):
+        assert len(np.unique(r)) > 50
+        s_abs = O.conv_f8_acc(x & 0x7F, wqq & 0x7F, s_, p_)
+        err = 2.0 ** -16 * np.abs(al).astype(np.float64)[None, :, None, None] * s_abs
+        _check_conv(g, r, err, 3e-3, what)
+    alone = ops.conv2d_nhwc_f8(xd, wdev, OC, 3, 2, 1, _cuda(alpha), _cuda(beta), relu=True).cpu().numpy()
+    assert np.array_equal(y.cpu().numpy(), alone)
+
+
+@pytest.mark.parametrize("N", [5, 37])
+def test_gap_and_fc_f8_bitexact(gpu, N):
+    """GAP (16-channel shuffle kernel) and FC (f64 MFMA kernel, exact sums):
+    bit-exact; N = 37 leaves partial 16-row FC tiles."""
+    from dlq_amd import ops
+    rng = np.random.default_rng(23 + N)
+    x = O.quantize_f32_f8(np.abs(rng.standard_normal((N, 512, 7, 7))).astype(np.float32) * 30, 1.0)
     k = O.gap_k_f8(0.02, 49, 0.015)
     g_ref, _ = O.gap_f8(x, k)
     g = ops.gap_nhwc_f8(_cuda(nchw_to_nhwc(x)), float(k)).cpu().numpy()
