@@ -270,6 +270,32 @@ def test_resnet18_batch_invariance_full_batch(gpu):
     assert np.array_equal(ref.view(np.int32), big[[0, 255]].view(np.int32))
 
 
+def test_resnet18_graph_replay_matches_launches(gpu, monkeypatch):
+    """The forward is captured once per (x, B, logits) into a hipGraph and
+    replayed (DLQ_GRAPH=1): a replay over NEW contents of the same input
+    buffer, and a re-capture for another batch size, equal the kernel-by-
+    kernel forward (the default) bit for bit."""
+    from dlq_amd.models import ResNet18Int8, synthetic_images
+    monkeypatch.setenv("DLQ_GRAPH", "1")
+    sd, scales = model_and_scales()
+    model = ResNet18Int8(sd, scales, max_batch=64)
+    x = synthetic_images(64, seed=3).cuda()
+    out = torch.empty((64, 1000), dtype=torch.float32, device="cuda")
+    got = []
+    for seed in (3, 4):  # capture, then replay over new pixels in the same buffer
+        x.copy_(synthetic_images(64, seed=seed).cuda())
+        got.append(model(x, out=out).cpu().numpy())
+    small = model(x[:5], out=out[:5]).cpu().numpy()  # another (x, B, logits): re-capture
+    monkeypatch.setenv("DLQ_GRAPH", "0")
+    ref = model(x).cpu().numpy()
+    x.copy_(synthetic_images(64, seed=3).cuda())
+    ref0 = model(x).cpu().numpy()
+    assert not np.array_equal(got[0], got[1])
+    assert np.array_equal(got[0].view(np.int32), ref0.view(np.int32))
+    assert np.array_equal(got[1].view(np.int32), ref.view(np.int32))
+    assert np.array_equal(small.view(np.int32), ref[:5].view(np.int32))
+
+
 def test_resnet18_half_batch_split_matches_single_stream(gpu, monkeypatch):
     """With DLQ_SPLIT=1, batches >= 64 run as two half-batches on two streams
     (separate halves of every workspace buffer); an odd batch must give the
