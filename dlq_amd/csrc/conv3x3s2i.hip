@@ -31,6 +31,7 @@
 // slice (tap 8 paired with zeros, 5 MFMAs per slice); the downsample's MFMA
 // takes the pair (tap 4, tap 5) with its A fragment's upper half zero, so only
 // the centre tap contributes.  B pairs stream through a 3-deep register ring.
+#include <cstdlib>
 #include <type_traits>
 
 #include "device_common.h"
@@ -48,7 +49,11 @@ constexpr int JDP = JSC + 16;         // downsample weight row pitch (48 B)
 constexpr int JNW = 8;                // waves
 constexpr int JOT = 128;              // output channels per item
 
-template <int OW, bool DS>
+// NSR > 0: resident weights (RW) -- all NSR stages' weight blocks are loaded
+// into LDS once per workgroup and only the patch streams through the ring.
+// Used when every item has the same output-channel tile (OCp == JOT: layer2.0,
+// whose 1024 items would otherwise re-stream the same 88 KB four times per CU).
+template <int OW, bool DS, int NSR = 0>
 struct JGeo {
   static constexpr int OH = OW, WI = 2 * OW, HI = 2 * OH;  // output / input geometry
   static constexpr int RPI = OW < 14 ? OW : (OW == 14 ? 14 : 7);  // output rows per chunk
@@ -59,21 +64,24 @@ struct JGeo {
   static constexpr int WB = JOT * JWP;                        // 38,912 = 38 pieces
   static constexpr int DB = JOT * JDP;                        // 6,144 = 6 pieces
   static constexpr int WP = (WB + (DS ? DB : 0)) / 1024;   // weight pieces (no downsample block without DS)
-  static constexpr int NPIECE = WP + PP;
-  static constexpr int OFF_P = WB + DB;                       // patch within a slot
+  static constexpr int WPC = NSR ? 0 : WP;                    // weight pieces per ring stage
+  static constexpr int NPIECE = WPC + PP;
+  static constexpr int W_ALL = NSR * WP * 1024;               // resident weights (stage j at j * WP KiB)
+  static constexpr int OFF_P = NSR ? W_ALL : WB + DB;         // slot 0's patch
   static constexpr int ZU = 2 * WI + 16;                      // zero units (kh rows x bank spread)
   static constexpr int OFF_Z = OFF_P + PP * 1024;
-  static constexpr int SLOT = OFF_Z + (ZU * 16 + 255) / 256 * 256;
-  static constexpr int OFF_AB = 2 * SLOT;                     // conv alpha/beta, then ds alpha/beta
+  static constexpr int ZB = (ZU * 16 + 255) / 256 * 256;
+  static constexpr int SLOT = NSR ? PP * 1024 + ZB : OFF_Z + ZB;  // ring slot stride
+  static constexpr int OFF_AB = NSR ? W_ALL + 2 * SLOT : 2 * SLOT;  // conv alpha/beta, then ds alpha/beta
   static_assert(IPI * RPI * OW == JL, "item = whole output rows");
   static_assert((WB + DB) % 1024 == 0, "weight blocks = whole DMA pieces");
   static_assert((2 * WI + OW) * 16 < 65536, "tap offsets fit the ds_read immediate");
 };
 
-template <int OW, int C, int OUT, bool DS, int NF, bool F8>
+template <int OW, int C, int OUT, bool DS, int NF, bool F8, bool RW>
 __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, int8_t* y_ds, int8_t* lds,
                                          int mt, int f0) {
-  using G = JGeo<OW, DS>;
+  using G = JGeo<OW, DS, RW ? C / JSC : 0>;
   constexpr int NS = C / JSC, OC = 2 * C;
   constexpr int DPW = (G::NPIECE + JNW - 1) / JNW;
   static_assert(DPW <= 18, "at most two DMA pieces per tap");
@@ -110,12 +118,12 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
 #pragma unroll
     for (int k = 0; k < DPW; ++k) {
       const int pc = piece_of(k);
-      if (pc < G::WB / 1024) {
+      if (pc < G::WPC && pc < G::WB / 1024) {
         doff[k] = ot * NS * G::WB + pc * 1024 + lane * 16;
-      } else if (pc < G::WP) {
+      } else if (pc < G::WPC) {
         doff[k] = ot * NS * G::DB + (pc - G::WB / 1024) * 1024 + lane * 16;
       } else {
-        const int u = (pc - G::WP) * 64 + lane;
+        const int u = (pc - G::WPC) * 64 + lane;
         const int plane = u >= G::UP ? 1 : 0, q = u - plane * G::UP;
         const int c = q / (G::IRC * G::WI), rem = q - c * (G::IRC * G::WI);
         const int r = rem / G::WI, pos = rem - r * G::WI;
@@ -132,13 +140,13 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     const int j = sc % NS;
     const int pc = piece_of(k);
     const int8_t* src;
-    if (pc < G::WB / 1024)
+    if (pc < G::WPC && pc < G::WB / 1024)
       src = a.w + (size_t)(doff[k] + j * G::WB);
-    else if (pc < G::WP)
+    else if (pc < G::WPC)
       src = w_ds + (size_t)(doff[k] + j * G::DB);
     else
       src = doff[k] < 0 ? g_zero_s2i + (lane & 3) * 16 : a.x + (size_t)(doff[k] + j * JSC);
-    const int dst = pc < G::WP ? pc * 1024 : G::OFF_P + (pc - G::WP) * 1024;
+    const int dst = pc < G::WPC ? pc * 1024 : G::OFF_P + (pc - G::WPC) * 1024;
     glds16_asm(src, lds32 + (s & 1) * G::SLOT + dst);
   };
   auto prep_for = [&](int s) {
@@ -170,6 +178,15 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
   Acc acc[NF], accd[DS ? NF : 1];
   int cur_ot = 0, cur_p0 = 0;
 
+  if constexpr (RW) {  // every stage's weight block (one output-channel tile), once
+    constexpr int NW = NS * G::WP;
+    for (int pc = wave; pc < NW; pc += JNW) {
+      const int j = pc / G::WP, q = pc - j * G::WP;
+      const int8_t* src = q < G::WB / 1024 ? a.w + (size_t)j * G::WB + q * 1024 + lane * 16
+                                           : w_ds + (size_t)j * G::DB + (q - G::WB / 1024) * 1024 + lane * 16;
+      glds16_asm(src, lds32 + pc * 1024);
+    }
+  }
   prep_for(0);
 #pragma unroll
   for (int k = 0; k < DPW; ++k) issue_piece(0, k);
@@ -200,7 +217,8 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
         left_off[f] += d;
       }
     }
-    const int8_t* abase = lds + sb + a_row;
+    const int wb = RW ? j * G::WP * 1024 : sb;  // this stage's weight block
+    const int8_t* abase = lds + wb + a_row;
     if constexpr (F8) {
       constexpr int NPAIR = 5, NM = NPAIR * NF, D = 3;
       auto ld_half = [&](int tap, int f) -> v4i {
@@ -227,7 +245,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
       for (int pr = 0; pr < NPAIR; ++pr) {
         if (pr + 1 < NPAIR) fa2[(pr + 1) & 1] = ld_a2(pr + 1);
         if constexpr (DS) {
-          if (pr == 1) fd2 = cat8(*(const v4i*)(lds + sb + d_row), v4i{0, 0, 0, 0});  // used with pair (4, 5)
+          if (pr == 1) fd2 = cat8(*(const v4i*)(lds + wb + d_row), v4i{0, 0, 0, 0});  // used with pair (4, 5)
         }
         const int k0 = 2 * pr * DPW / 9, k1 = (2 * pr + 2 < 9 ? 2 * pr + 2 : 9) * DPW / 9;
         if (more && !(a.dbg & 2)) {
@@ -260,7 +278,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
       const int bu = tap & 1;
       if (tap + 1 < 9) fa[bu ^ 1] = *(const v4i*)(abase + (tap + 1) * 32);
       if constexpr (DS) {
-        if (tap == 3) fd = *(const v4i*)(lds + sb + d_row);  // the downsample's A fragment, used at tap 4
+        if (tap == 3) fd = *(const v4i*)(lds + wb + d_row);  // the downsample's A fragment, used at tap 4
       }
       const int k0 = tap * DPW / 9, k1 = (tap + 1) * DPW / 9;
       if (more && !(a.dbg & 2)) {  // dbg 2: timing experiment without the DMA
@@ -362,10 +380,10 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
 }
 
 // OUT: 0 = int8 (fused epilogues), 2 = int32 conv1 accumulators (DS = false).
-template <int OW, int C, int OUT, bool DS, bool F8>
+template <int OW, int C, int OUT, bool DS, bool F8, bool RW = false>
 __global__ __launch_bounds__(JNW * 64, 1) void conv3x3s2i_kernel(ConvArgs a, const int8_t* w_ds, const float* al_ds,
                                                                  const float* be_ds, int8_t* y_ds) {
-  using G = JGeo<OW, DS>;
+  using G = JGeo<OW, DS, RW ? C / JSC : 0>;
   constexpr int OC = 2 * C;
   constexpr int LDS_TOTAL = G::OFF_AB + (DS ? 4 : 2) * OC * 4;
   static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
@@ -389,9 +407,9 @@ __global__ __launch_bounds__(JNW * 64, 1) void conv3x3s2i_kernel(ConvArgs a, con
   __syncthreads();
   const int wave = tid >> 6;
   if (wave < 4)
-    s2i_body<OW, C, OUT, DS, 4, F8>(a, w_ds, y_ds, lds, wave & 3, 0);
+    s2i_body<OW, C, OUT, DS, 4, F8, RW>(a, w_ds, y_ds, lds, wave & 3, 0);
   else
-    s2i_body<OW, C, OUT, DS, 3, F8>(a, w_ds, y_ds, lds, wave & 3, 4);
+    s2i_body<OW, C, OUT, DS, 3, F8, RW>(a, w_ds, y_ds, lds, wave & 3, 4);
 }
 
 int num_cus_s2i() {
@@ -415,6 +433,17 @@ hipError_t launch_j(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, c
     hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 2, false, F8>), grid, block, 0, s, a, nullptr, nullptr, nullptr,
                        nullptr);
   } else if (w_ds) {
+    if constexpr (OW == 28 && C == 64) {  // layer2.0: one output-channel tile -> resident weights
+      static const bool ring = [] {
+        const char* e = std::getenv("DLQ_S2_RING");
+        return e && e[0] == '1';
+      }();
+      if (a.OCp == JOT && !ring) {
+        hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true, F8, true>), grid, block, 0, s, a, w_ds, al_ds, be_ds,
+                           y_ds);
+        return hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true, F8>), grid, block, 0, s, a, w_ds, al_ds, be_ds, y_ds);
   } else {
     hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, false, F8>), grid, block, 0, s, a, nullptr, nullptr, nullptr,
