@@ -69,6 +69,41 @@ def shard_gather(forward, x_local, world, out_global=None):
     return out_global
 
 
+class GatherPipeline:
+    """The data-parallel step with the exchange overlapped: step i runs its
+    forward into logits slot i % 2 and starts an ASYNC all-gather of that slot
+    (RCCL runs it on its own stream); step i+1's forward proceeds into the other
+    slot while it is in flight, and a slot is reused only after its previous
+    gather has been waited on.  finish() waits for every gather in flight, so
+    a timed region that ends with finish() + synchronize covers every step's
+    forward AND its all-gather.  world == 1: no exchange."""
+
+    def __init__(self, forward_into, B, world, device, depth=2):
+        self.forward_into, self.world, self.depth = forward_into, world, depth
+        self.logits = [torch.empty((B, 1000), dtype=torch.float32, device=device) for _ in range(depth)]
+        self.out = ([torch.empty((world * B, 1000), dtype=torch.float32, device=device) for _ in range(depth)]
+                    if world > 1 else self.logits)
+        self.work = [None] * depth
+        self.i = 0
+
+    def step(self, x_local):
+        k = self.i % self.depth
+        self.i += 1
+        if self.work[k] is not None:
+            self.work[k].wait()
+            self.work[k] = None
+        self.forward_into(x_local, self.logits[k])
+        if self.world > 1:
+            self.work[k] = dist.all_gather_into_tensor(self.out[k], self.logits[k], async_op=True)
+        return k
+
+    def finish(self):
+        for k, w in enumerate(self.work):
+            if w is not None:
+                w.wait()
+                self.work[k] = None
+
+
 def pmc_traffic(kernel_family):
     """HBM bytes per launch of a kernel family from the committed rocprofv3 PMC
     summary (profiles/*pmc_traffic.json, written by tools/pmc_traffic.py:
@@ -144,19 +179,21 @@ def main():
     std = torch.tensor([0.229, 0.224, 0.225], device=dev).view(1, 3, 1, 1)
     x = ((pix.float() / 255.0 - mean) / std).contiguous()
     del pix
-    logits = torch.empty((B, 1000), dtype=torch.float32, device=dev)
-    gathered = torch.empty((world * B, 1000), dtype=torch.float32, device=dev) if world > 1 else None
+    pipe = GatherPipeline(lambda xx, out: model.forward(xx, out), B, world, dev)
+    logits = pipe.logits[0]
     fwd = lambda xx: model.forward(xx, logits)  # noqa: E731
 
     for _ in range(args.warmup):
-        shard_gather(fwd, x, world, gathered)
+        pipe.step(x)
+    pipe.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        shard_gather(fwd, x, world, gathered)
+        pipe.step(x)
+    pipe.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
