@@ -27,3 +27,11 @@ python3 tools/fwdstats.py $(find gpurun_out/kt -name '*kernel_trace.csv' | head 
 tail -19 gpurun_out/${R}_per_position.txt
 timeout -k 10 300 python3 bench.py > gpurun_out/${R}_bench_plain.log 2>&1; rc=$?; echo "bench(plain) rc=$rc"
 grep '^{"metric"' gpurun_out/${R}_bench_plain.log > gpurun_out/${R}_bench.json; cut -c 1-200 gpurun_out/${R}_bench.json
+# fp8 (configs[4]): kernel stats of the same bench command under rocprofv3, then a plain run
+rm -rf gpurun_out/kt8
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt8 -o run -- python3 bench.py --precision fp8 --cpu-baseline-images 0 --torch-cpu-images 0 > gpurun_out/${R}_f8_bench_under_rocprof.log 2>&1; rc=$?; echo "f8 bench(rocprof) rc=$rc"
+[ $rc -eq 0 ] || exit $rc
+cp $(find gpurun_out/kt8 -name '*kernel_stats.csv' | head -1) gpurun_out/${R}_f8_kernel_stats.csv
+timeout -k 10 300 python3 bench.py --precision fp8 --cpu-baseline-images 0 --torch-cpu-images 0 > gpurun_out/${R}_f8_bench_plain.log 2>&1; rc=$?; echo "f8 bench(plain) rc=$rc"
+grep '^{"metric"' gpurun_out/${R}_f8_bench_plain.log > gpurun_out/${R}_f8_bench.json; cut -c 1-200 gpurun_out/${R}_f8_bench.json
+exit $rc
