@@ -69,7 +69,14 @@ struct IGeo {
   static constexpr int OT = W == 7 ? 64 : 128;        // output channels per item
   static constexpr int MT = OT / 32;                  // oc tiles per item
   static constexpr int RW = W;                        // patch row pitch in units (compact rows)
-  static constexpr int UP = (IPI * (RPI + 2) * RW + 15) / 16 * 16;  // units per 16-channel plane
+  // Chunk pitch in units: >= the chunk's RPI + 2 rows and == RPI * W (mod 16),
+  // so unit - pixel is the same mod 16 for every pixel of an item and a
+  // ds_read_b128 lane group (16 consecutive pixels) hits 16 distinct bank
+  // quads even across a chunk boundary (compact chunks: 26 % of the W = 7
+  // launch's LDS cycles were bank conflicts, SQ_LDS_BANK_CONFLICT).
+  static constexpr int CS0 = (RPI + 2) * RW;
+  static constexpr int CS = CS0 + (((RPI * W - CS0) % 16) + 16) % 16;
+  static constexpr int UP = (IPI * CS + 15) / 16 * 16;  // units per 16-channel plane
   static constexpr int PP = (2 * UP + 63) / 64;       // patch DMA pieces (1 KiB)
   static constexpr int ZU = 2 * W + 16;               // zero units read by the edge columns' side taps
   static constexpr int WB = OT * IPITCH;              // weight bytes per stage
@@ -166,11 +173,12 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       } else {
         const int u = (pc - G::WP) * 64 + lane;
         const int plane = u >= G::UP ? 1 : 0, q = u - plane * G::UP;
-        const int c = q / ((G::RPI + 2) * G::RW), rem = q - c * ((G::RPI + 2) * G::RW);
+        const int c = q / G::CS, rem = q - c * G::CS;
         const int r = rem / G::RW, iw = rem - r * G::RW;
         const int gr = R0 + c * G::RPI;  // chunk's first global output row
         const int n = gr / H, ih = gr - n * H + r - 1;
-        const bool ok = u < 2 * G::UP && n < a.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        const bool ok = u < 2 * G::UP && c < G::IPI && r < G::RPI + 2 && n < a.N && (unsigned)ih < (unsigned)H &&
+                        (unsigned)iw < (unsigned)W;
         doff[k] = ok ? ((n * H + ih) * W + iw) * C + plane * 16 : -1;
       }
     }
@@ -205,7 +213,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     lp = lp < IL ? lp : IL - 1;
     const int c = lp / (G::RPI * W), rem = lp - c * (G::RPI * W);
     const int r = rem / W, ow = rem - r * W;
-    const int bu = (c * (G::RPI + 2) + r) * G::RW + ow;  // tap (kh 0, kw 1): the pixel above
+    const int bu = c * G::CS + r * G::RW + ow;  // tap (kh 0, kw 1): the pixel above
     const int mid = G::WB + lh * G::UP * 16 + bu * 16;
     col_off[1][f] = mid;
     col_off[0][f] = ow == 0 ? G::OFF_Z + ((bu - 1) & 15) * 16 : mid - 16;

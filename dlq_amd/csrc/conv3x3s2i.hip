@@ -317,7 +317,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     }
     }  // int8 MFMA loop
 
-    if (j != NS - 1) continue;
+    if (j != NS - 1 || (a.dbg & 4)) continue;  // dbg 4: timing experiment without the epilogues
     // ---- fused epilogues of the item ----
     if constexpr (OUT == 2) {
 #pragma unroll
