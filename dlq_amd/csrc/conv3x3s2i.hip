@@ -59,7 +59,10 @@ struct JGeo {
   static constexpr int RPI = OW < 14 ? OW : (OW == 14 ? 14 : 7);  // output rows per chunk
   static constexpr int IPI = JL / (RPI * OW);                 // chunks (images) per item
   static constexpr int IRC = 2 * RPI + 1;                     // input rows per chunk
-  static constexpr int UP = (IPI * IRC * WI + 15) / 16 * 16;  // units per 16-channel plane
+  // chunk pitch in units: one spare unit for the four 7x7 images of OW = 7 so
+  // that no bank quad serves more than 14 of an item's pixels (PixPerm)
+  static constexpr int CS = IRC * WI + (OW == 7 ? 1 : 0);
+  static constexpr int UP = (IPI * CS + 15) / 16 * 16;        // units per 16-channel plane
   static constexpr int PP = (2 * UP + 63) / 64;               // patch DMA pieces
   static constexpr int WB = JOT * JWP;                        // 38,912 = 38 pieces
   static constexpr int DB = JOT * JDP;                        // 6,144 = 6 pieces
@@ -77,6 +80,60 @@ struct JGeo {
   static_assert((WB + DB) % 1024 == 0, "weight blocks = whole DMA pieces");
   static_assert((2 * WI + OW) * 16 < 65536, "tap offsets fit the ds_read immediate");
 };
+
+// Pixel -> lane assignment.  A B-fragment ds_read_b128 is served in 16-lane
+// groups ({0-3,12-15,20-27} and {4-11,16-19,28-31} of each lane half), and a
+// group is conflict-free only if its 16 pixels' tap units fall in 16
+// distinct bank quads (unit mod 16).  In row order the stride-2 patch rows
+// (2 input rows of 2*OW units per output row of OW pixels) shift that
+// residue at every row end: 33-42 % of these launches' LDS cycles were bank
+// conflicts (SQ_LDS_BANK_CONFLICT).  The D tile's pixel set is free, so the
+// item's 196 pixels are dealt to the 7 tiles x 2 groups by residue: the k-th
+// pixel of residue q goes to group k, lane slot q (every residue occurs <= 14
+// times); the 28 spare lanes re-read a donor pixel of the missing residue and
+// are flagged (0x4000) so the epilogue drops them.  Every tap adds the same
+// unit offset to all lanes, so all taps stay conflict-free.
+struct PixPerm {
+  short px[7 * 32];
+};
+
+template <int OW>
+constexpr PixPerm make_perm() {
+  using G = JGeo<OW, true>;
+  constexpr int LA[16] = {0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27};
+  constexpr int LB[16] = {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31};
+  PixPerm t{};
+  int cnt[16] = {}, donor[16] = {};
+  for (int q = 0; q < 16; ++q) donor[q] = -1;
+  for (int i = 0; i < 7 * 32; ++i) t.px[i] = -1;
+  for (int p = 0; p < JL; ++p) {
+    const int c = p / (G::RPI * OW), rem = p - c * (G::RPI * OW), r = rem / OW, ow = rem - r * OW;
+    const int q = (c * G::CS + 2 * r * G::WI + ow) & 15;
+    const int k = cnt[q]++;  // group k: tile k / 2, lane half-group k % 2
+    if (donor[q] < 0) donor[q] = p;
+    t.px[(k / 2) * 32 + ((k & 1) ? LB[q] : LA[q])] = (short)p;
+  }
+  for (int tile = 0; tile < 7; ++tile)
+    for (int q = 0; q < 16; ++q) {
+      if (t.px[tile * 32 + LA[q]] < 0) t.px[tile * 32 + LA[q]] = (short)(donor[q] | 0x4000);
+      if (t.px[tile * 32 + LB[q]] < 0) t.px[tile * 32 + LB[q]] = (short)(donor[q] | 0x4000);
+    }
+  return t;
+}
+
+__constant__ PixPerm g_perm28 = make_perm<28>();
+__constant__ PixPerm g_perm14 = make_perm<14>();
+__constant__ PixPerm g_perm7 = make_perm<7>();
+
+template <int OW>
+__device__ __forceinline__ int perm_at(int slot) {
+  if constexpr (OW == 28)
+    return g_perm28.px[slot];
+  else if constexpr (OW == 14)
+    return g_perm14.px[slot];
+  else
+    return g_perm7.px[slot];
+}
 
 template <int OW, int C, int OUT, bool DS, int NF, bool F8, bool RW>
 __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, int8_t* y_ds, int8_t* lds,
@@ -125,12 +182,12 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
       } else {
         const int u = (pc - G::WPC) * 64 + lane;
         const int plane = u >= G::UP ? 1 : 0, q = u - plane * G::UP;
-        const int c = q / (G::IRC * G::WI), rem = q - c * (G::IRC * G::WI);
+        const int c = q / G::CS, rem = q - c * G::CS;
         const int r = rem / G::WI, pos = rem - r * G::WI;
         const int iw = pos < OW ? 2 * pos : 2 * (pos - OW) + 1;  // de-interleaved: even cols, then odd
         const int gr = R0 + c * G::RPI;  // chunk's first global output row
         const int n = gr / G::OH, ih = 2 * (gr - n * G::OH) - 1 + r;
-        const bool ok = u < 2 * G::UP && n < a.N && (unsigned)ih < (unsigned)G::HI;
+        const bool ok = u < 2 * G::UP && c < G::IPI && r < G::IRC && n < a.N && (unsigned)ih < (unsigned)G::HI;
         doff[k] = ok ? ((n * G::HI + ih) * G::WI + iw) * C + plane * 16 : -1;
       }
     }
@@ -166,11 +223,10 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
   int mid_off[NF], left_off[NF];
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
-    int lp = (f0 + f) * 32 + lr;
-    lp = lp < JL ? lp : JL - 1;
+    const int lp = perm_at<OW>((f0 + f) * 32 + lr) & 0x3fff;
     const int c = lp / (G::RPI * OW), rem = lp - c * (G::RPI * OW);
     const int r = rem / OW, ow = rem - r * OW;
-    const int bu = (c * G::IRC + 2 * r) * G::WI + ow;  // E[ow] of input row 2r-1
+    const int bu = c * G::CS + 2 * r * G::WI + ow;  // E[ow] of input row 2r-1
     mid_off[f] = G::OFF_P + lh * G::UP * 16 + bu * 16;
     left_off[f] = ow == 0 ? G::OFF_Z + ((bu + OW - 1) & 15) * 16 : mid_off[f] + (OW - 1) * 16;
   }
@@ -322,8 +378,8 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     if constexpr (OUT == 2) {
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
-        const int lp = (f0 + f) * 32 + lr, p = cur_p0 + lp;
-        const bool keep = lp < JL && p < a.P;
+        const int e = perm_at<OW>((f0 + f) * 32 + lr), p = cur_p0 + (e & 0x3fff);
+        const bool keep = !(e & 0x4000) && p < a.P;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int oc = cur_ot * JOT + mt * 32 + 8 * g + 4 * lh;
@@ -364,8 +420,8 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
           }
           swap32(q[0], q[2]);
           swap32(q[1], q[3]);
-          const int lp = (f0 + f) * 32 + lr, p = cur_p0 + lp;
-          const bool keep = lp < JL && p < a.P;
+          const int e = perm_at<OW>((f0 + f) * 32 + lr), p = cur_p0 + (e & 0x3fff);
+          const bool keep = !(e & 0x4000) && p < a.P;
           v4i* dst = keep ? (v4i*)(out + (size_t)p * a.OC + cur_ot * JOT + mt * 32 + lh * 16)
                           : (v4i*)(g_trash_s2i + lane * 16);
           *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
