@@ -5,6 +5,7 @@
 # traffic summary) and the kernel stats come from the same process and the
 # per-kernel averages agree; finally a plain bench run.
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${ROUND:-r01}_smoke.log 2>&1 || exit 1; tail -1 gpurun_out/${ROUND:-r01}_smoke.log
 R=${ROUND:-r01}
 set -o pipefail
 timeout -k 10 600 python -u -m pytest tests/ -q -m gpu -x --timeout 120 --timeout-method thread > gpurun_out/${R}_gpu_tests.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -1 gpurun_out/${R}_gpu_tests.log
