@@ -160,6 +160,12 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     return pc >= G::NPIECE ? pc - G::NPIECE : pc;  // past the end: re-issue an earlier piece
   };
   auto prep_issue = [&](int li) {
+    // lane is made opaque here so the compiler recomputes the per-piece lane
+    // decompositions (a few VALU ops per item) instead of hoisting them out
+    // of the stage loop: hoisted, they were spilled to scratch and reloaded
+    // as ~28 serialised scratch_load + s_waitcnt vmcnt(0) at every item change
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
     int ot, p0;
     item_of(li, ot, p0);
     const int R0 = p0 / W;  // first global output row of the item
@@ -360,7 +366,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     }  // int8 MFMA loop
 
     ISTAMP(2 + 2 * s);
-    if (j != NS - 1) continue;
+    if (j != NS - 1 || (a.dbg & 4)) continue;  // dbg 4: timing experiment without the epilogue
     // ---- fused epilogue of the item ----
     if constexpr (OUT == 2) {
 #pragma unroll

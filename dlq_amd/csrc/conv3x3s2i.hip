@@ -169,6 +169,12 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     return pc >= G::NPIECE ? pc - G::NPIECE : pc;
   };
   auto prep_issue = [&](int li) {
+    // lane is made opaque here so the compiler recomputes the per-piece lane
+    // decompositions (a few VALU ops per item) instead of hoisting them out
+    // of the stage loop: hoisted, they were spilled to scratch and reloaded
+    // as ~28 serialised scratch_load + s_waitcnt vmcnt(0) at every item change
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
     int ot, p0;
     item_of(li, ot, p0);
     const int R0 = p0 / OW;  // first global output row
