@@ -357,6 +357,17 @@ int dlq_gap_nhwc_s8(const int8_t* x, int N, int C, int HW, float k, int8_t* y, v
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, hipGetErrorString(e));
 }
 
+int dlq_gap_fc_s8(const int8_t* x, int N, int C, int HW, float k, const int8_t* w_packed, int OC,
+                  const float* alpha, const float* beta, float* y, void* stream) {
+  if (C != 512 || HW <= 0 || HW > 56 || N < 0 || OC <= 0) return fail(DLQ_ERR_ARG, "gap_fc: bad args (C == 512, HW <= 56)");
+  if (N == 0) return DLQ_OK;
+  if (!x || !w_packed || !alpha || !beta || !y) return fail(DLQ_ERR_ARG, "gap_fc: null pointer");
+  if ((long long)N * HW * C >= (1LL << 31) || (long long)N * OC * 4 >= (1LL << 31))
+    return fail(DLQ_ERR_ARG, "gap_fc: tensor exceeds 2^31 bytes; split the batch");
+  hipError_t e = launch_gap_fc(x, N, C, HW, k, w_packed, OC, alpha, beta, y, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("gap_fc launch: ") + hipGetErrorString(e));
+}
+
 int dlq_im2col_nchw_s8(const int8_t* x, int N, int C, int H, int W, int kH, int kW, int sH, int sW,
                        int pH, int pW, int8_t* col, void* stream) {
   if (!x || !col || N < 0 || C <= 0 || kH <= 0 || kW <= 0 || sH <= 0 || sW <= 0)

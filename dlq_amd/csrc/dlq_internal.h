@@ -78,6 +78,8 @@ hipError_t launch_gap(const int8_t* x, int N, int C, int HW, float k, int8_t* y,
 hipError_t launch_gap4(const int8_t* x, int N, int C, int HW, float k, int8_t* y, hipStream_t s);  // C % 4 == 0
 hipError_t launch_linear(const int8_t* x, int N, int K, const int8_t* w, int OC, const float* alpha,
                          const float* beta, int relu, int out_kind, void* y, hipStream_t s);
+hipError_t launch_gap_fc(const int8_t* x, int N, int C, int HW, float k, const int8_t* w, int OC,
+                         const float* alpha, const float* beta, float* y, hipStream_t s);  // C == 512, HW <= 56
 hipError_t launch_im2col_nchw(const int8_t* x, int N, int C, int H, int W, int kH, int kW, int sH,
                               int sW, int pH, int pW, int8_t* col, hipStream_t s);
 

@@ -227,6 +227,13 @@ bool unfused_stem() {
   return v;
 }
 
+// DLQ_HEAD_SPLIT=1 (read at every call): GAP and FC as two launches
+// (gap16_kernel + linear_kernel) instead of the fused gap_fc_kernel.
+bool head_split() {
+  const char* e = std::getenv("DLQ_HEAD_SPLIT");
+  return e && e[0] == '1';
+}
+
 // conv2d_nchw_im2col_gemm + bn_launch (+ add_inplace + relu_forward) of the
 // reference, as one implicit-GEMM launch with the epilogue fused.
 int conv2d_nhwc_s8(const dlq_resnet18* m, const ConvLayer& c, const int8_t* x, int N, int H, int W,
@@ -978,6 +985,11 @@ int forward_pass(dlq_resnet18* m, const float* x, int B, float* logits, hipStrea
   const std::string last = m->convs[m->blocks.back().c2].site;
   const float k = (m->scales.at(last) / (float)(H * W)) / m->scales.at("gap");
   if ((rc = mark(m, s, DLQ_FAM_GAP))) return rc;
+  if (!m->keep && !head_split()) {  // one launch (head.hip gap_fc_kernel); the GAP codes stay on chip
+    rc = dlq_gap_fc_s8(cur, B, 512, H * W, k, m->fc_w, 1000, m->fc_alpha, m->fc_beta, logits, stream);
+    if (rc) return rc;
+    return mark(m, s, -1);
+  }
   rc = dlq_gap_nhwc_s8(cur, B, 512, H * W, k, gq, stream);
   if (rc) return rc;
   if (record) m->stage["gap"] = {gq, nB * 512};
@@ -1195,9 +1207,14 @@ int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes)
     macs[conv_family(c2, OH)] += mac2;
     bytes[conv_family(c2, OH)] += out + out + out;  // input, residual, output
   }
-  macs[DLQ_FAM_FC] = 512.0 * 1000;
-  bytes[DLQ_FAM_FC] = 512.0 + 4000.0;
-  bytes[DLQ_FAM_GAP] = 7.0 * 7 * 512 + 512;
+  if (head_split()) {
+    macs[DLQ_FAM_FC] = 512.0 * 1000;
+    bytes[DLQ_FAM_FC] = 512.0 + 4000.0;
+    bytes[DLQ_FAM_GAP] = 7.0 * 7 * 512 + 512;
+  } else {  // gap_fc_kernel: layer4 output in, fp32 logits out
+    macs[DLQ_FAM_GAP] = 512.0 * 1000;
+    bytes[DLQ_FAM_GAP] = 7.0 * 7 * 512 + 4000.0;
+  }
   return DLQ_OK;
 }
 

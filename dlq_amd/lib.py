@@ -22,7 +22,7 @@ DLQ_OUT_S8, DLQ_OUT_F32, DLQ_OUT_S32 = 0, 1, 2
 DLQ_PREC_INT8, DLQ_PREC_FP8 = 0, 1
 # kernel families of dlq_resnet18_timing (include/dlq.h DLQ_FAM_*)
 FAMILIES = ["stem_fused_kernel", "block_l1_kernel (layer1 block)", "conv3x3s2i_kernel (+downsample)",
-            "conv3x3i_kernel (layer2-4 s1)", "gap16_kernel", "linear_kernel (fc)", "other",
+            "conv3x3i_kernel (layer2-4 s1)", "head: gap_fc_kernel (int8 GAP+FC) / gap16 (fp8, split)", "linear_kernel (fc: fp8 / split head)", "other",
             "conv_s8_kernel fp8 (all convs, fp8 path)"]
 
 
@@ -72,6 +72,7 @@ _SIGS = {
     "dlq_linear_s8": ([_vp, _i, _i, _vp, _i, _vp, _vp, _i, _i, _vp, _vp], _i),
     "dlq_maxpool2d_3x3_s2p1_nhwc_s8": ([_vp, _i, _i, _i, _i, _vp, _vp], _i),
     "dlq_gap_nhwc_s8": ([_vp, _i, _i, _i, _f, _vp, _vp], _i),
+    "dlq_gap_fc_s8": ([_vp, _i, _i, _i, _f, _vp, _i, _vp, _vp, _vp, _vp], _i),
     "dlq_im2col_nchw_s8": ([_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp], _i),
     "dlq_resnet18_create": ([C.POINTER(_vp)], _i),
     "dlq_resnet18_destroy": ([_vp], None),

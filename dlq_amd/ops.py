@@ -221,6 +221,19 @@ def gap_nhwc_s8(x: torch.Tensor, k: float) -> torch.Tensor:
     return y
 
 
+def gap_fc_s8(x: torch.Tensor, k: float, w_packed: torch.Tensor, OC: int, alpha: torch.Tensor,
+              beta: torch.Tensor) -> torch.Tensor:
+    """The network head in one launch (include/dlq.h dlq_gap_fc_s8): fp32
+    logits [N, OC] from NHWC int8 x[N, H, W, 512], equal bit for bit to
+    ``linear_s8(gap_nhwc_s8(x, k), w_packed, OC, alpha, beta)``."""
+    _dev(x, torch.int8)
+    N, H, W, Cc = x.shape
+    y = torch.empty((N, OC), dtype=torch.float32, device=x.device)
+    check(lib.dlq_gap_fc_s8(ptr(x), N, Cc, H * W, float(k), ptr(w_packed), OC, ptr(alpha), ptr(beta), ptr(y),
+                            stream_handle()), "gap_fc")
+    return y
+
+
 def im2col_nchw_s8(x: torch.Tensor, k: int, stride: int, pad: int) -> torch.Tensor:
     _dev(x, torch.int8)
     N, Cc, H, W = x.shape

@@ -245,6 +245,13 @@ int dlq_maxpool2d_3x3_s2p1_nhwc_s8(const int8_t* x, int N, int C, int H, int W, 
  * exact int32 sum, then clamp(rne(float(sum) * k)), k = s_in/HW/s_out. */
 int dlq_gap_nhwc_s8(const int8_t* x, int N, int C, int HW, float k, int8_t* y, void* stream);
 
+/* The network head in one launch: dlq_gap_nhwc_s8 followed by
+ * dlq_linear_s8(..., relu 0, DLQ_OUT_F32) (gap_global_ref + fc_forward,
+ * RK/runtime/infer_e2e.cu:417-433), bit-identical logits, the int8 GAP codes
+ * kept on chip.  C must be 512 (= K) and HW <= 56 (DLQ_ERR_ARG otherwise). */
+int dlq_gap_fc_s8(const int8_t* x, int N, int C, int HW, float k, const int8_t* w_packed, int OC,
+                  const float* alpha, const float* beta, float* y, void* stream);
+
 /* im2col in the reference's row order r = c*kH*kW + kh*kW + kw
  * (RK/kernels/im2col.cu:5-58) on int8 NCHW, batch honoured: col[N][K][OH*OW].
  * Parity/debug only -- the conv kernel gathers patches implicitly. */

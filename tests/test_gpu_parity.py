@@ -216,6 +216,56 @@ def test_maxpool_and_gap_bitexact(gpu):
     assert np.array_equal(ggot, gref)
 
 
+@pytest.mark.parametrize("N,HW,OC", [(1, 49, 1000), (5, 49, 1000), (256, 49, 1000), (7, 1, 1000), (6, 56, 64),
+                                     (3, 17, 10)])
+def test_gap_fc_fused_head_bitexact(gpu, N, HW, OC):
+    """gap_fc_kernel (one launch) == oracle GAP then FC, bit for bit, on ragged
+    image groups (N % 4 != 0), HW from 1 to its 56 maximum and OC tails."""
+    from dlq_amd import ops
+    from tests.helpers import golden
+    rng = np.random.default_rng(N * 131 + HW)
+    W = golden("fc.weight.bin", (1000, 512))[:OC]  # the reference's real FC weights (tmp_e2e/)
+    bias = golden("fc.bias.bin")[:OC]
+    wq, sw = O.quantize_weights_s8(W)
+    x = rand_s8(rng, (N, 512, 1, HW), lo=0)  # post-ReLU int8 layer4 output, NCHW
+    k = O.gap_k(0.05, HW, 0.011)
+    g, _ = O.gap_s8(x, k)
+    alpha = O.fc_alpha(0.011, sw)
+    ref, _ = O.fc_s8(g, wq, alpha, bias)
+    ocp = ops.packed_oc(OC)
+    packed = _cuda(ops.pack_linear_weights(wq))
+    a, b = _cuda(ops.pad_vec(alpha, ocp)), _cuda(ops.pad_vec(bias, ocp))
+    xh = _cuda(nchw_to_nhwc(x))
+    got = ops.gap_fc_s8(xh, float(k), packed, OC, a, b).cpu().numpy()
+    assert np.array_equal(got.view(np.int32), ref.view(np.int32))
+    split = ops.linear_s8(ops.gap_nhwc_s8(xh, float(k)), packed, OC, a, b).cpu().numpy()
+    assert np.array_equal(got.view(np.int32), split.view(np.int32))
+
+
+def test_gap_fc_rejects_unsupported_shapes(gpu):
+    from dlq_amd import ops
+    from dlq_amd.lib import DLQError
+    x = torch.zeros((2, 8, 8, 512), dtype=torch.int8, device="cuda")  # HW 64 > 56
+    w = torch.zeros(1024 * 512, dtype=torch.int8, device="cuda")
+    v = torch.zeros(1024, dtype=torch.float32, device="cuda")
+    with pytest.raises(DLQError):
+        ops.gap_fc_s8(x, 0.1, w, 1000, v, v)
+    with pytest.raises(DLQError):
+        ops.gap_fc_s8(torch.zeros((2, 7, 7, 256), dtype=torch.int8, device="cuda"), 0.1, w, 1000, v, v)
+
+
+def test_resnet18_fused_head_matches_split_head(gpu, monkeypatch):
+    """B=256 forward with the fused head (default) == DLQ_HEAD_SPLIT=1."""
+    from dlq_amd.models import ResNet18Int8, synthetic_images
+    sd, scales = model_and_scales()
+    x = synthetic_images(256, seed=21).cuda()
+    model = ResNet18Int8(sd, scales, max_batch=256)
+    fused = model(x).cpu().numpy()
+    monkeypatch.setenv("DLQ_HEAD_SPLIT", "1")
+    split = model(x).cpu().numpy()
+    assert np.array_equal(fused.view(np.int32), split.view(np.int32))
+
+
 def test_im2col_reference_order_bitexact(gpu):
     from dlq_amd import ops
     rng = np.random.default_rng(9)
