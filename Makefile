@@ -7,7 +7,7 @@ ARCH ?= gfx950
 # -ffp-contract=off: the fp32 epilogue/host-prep op order is part of the
 # numerics contract (every fused multiply-add is an explicit fmaf).
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result
-SRC = dlq_amd/csrc/kernels.hip dlq_amd/csrc/conv3x3.hip dlq_amd/csrc/conv3x3w.hip dlq_amd/csrc/conv3x3i.hip dlq_amd/csrc/conv3x3s2.hip dlq_amd/csrc/conv3x3s2i.hip dlq_amd/csrc/block_l1.hip dlq_amd/csrc/stem.hip dlq_amd/csrc/head.hip dlq_amd/csrc/layerops.hip dlq_amd/csrc/preproc.hip dlq_amd/csrc/fp8.hip dlq_amd/csrc/capi.cpp dlq_amd/csrc/resnet18.cpp dlq_amd/csrc/mlp.cpp
+SRC = dlq_amd/csrc/kernels.hip dlq_amd/csrc/conv3x3.hip dlq_amd/csrc/conv3x3i.hip dlq_amd/csrc/conv3x3s2i.hip dlq_amd/csrc/block_l1.hip dlq_amd/csrc/stem.hip dlq_amd/csrc/head.hip dlq_amd/csrc/layerops.hip dlq_amd/csrc/gemm.hip dlq_amd/csrc/preproc.hip dlq_amd/csrc/fp8.hip dlq_amd/csrc/ref_f32.hip dlq_amd/csrc/capi.cpp dlq_amd/csrc/resnet18.cpp dlq_amd/csrc/mlp.cpp dlq_amd/csrc/wpack.cpp
 HDR = include/dlq.h dlq_amd/csrc/dlq_internal.h dlq_amd/csrc/device_common.h
 
 all: dlq_amd/libdlq.so bin/dlq_e2e oracle
@@ -20,7 +20,7 @@ build/%.o: dlq_amd/csrc/%.cpp $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -x hip -c -o $@ $<
 
-dlq_amd/libdlq.so: build/kernels.o build/conv3x3.o build/conv3x3w.o build/conv3x3i.o build/conv3x3s2.o build/conv3x3s2i.o build/block_l1.o build/stem.o build/head.o build/layerops.o build/preproc.o build/fp8.o build/capi.o build/resnet18.o build/mlp.o
+dlq_amd/libdlq.so: build/kernels.o build/conv3x3.o build/conv3x3i.o build/conv3x3s2i.o build/block_l1.o build/stem.o build/head.o build/layerops.o build/gemm.o build/preproc.o build/fp8.o build/ref_f32.o build/capi.o build/resnet18.o build/mlp.o build/wpack.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 bin/dlq_e2e: dlq_amd/csrc/main_e2e.cpp dlq_amd/libdlq.so include/dlq.h

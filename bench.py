@@ -33,10 +33,14 @@ def parse():
                     help="forwards of the per-kernel event-timing pass after the timed region")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
-    ap.add_argument("--cpu-baseline-images", type=int, default=24,
-                    help="bounded sample for the CPU oracle baseline (0 = skip)")
-    ap.add_argument("--torch-cpu-images", type=int, default=8,
-                    help="images for the torch fp32 CPU reference timing (0 = skip)")
+    ap.add_argument("--cpu-baseline-images", type=int, default=256,
+                    help="batch of the torch fp32 CPU baseline (the reported cpu_baseline; 0 = skip)")
+    ap.add_argument("--cpu-baseline-iters", type=int, default=3, help="timed iterations of that batch")
+    ap.add_argument("--oracle-images", type=int, default=12,
+                    help="bounded sample for the 1-thread C oracle timing (extra key; 0 = skip)")
+    ap.add_argument("--extras", type=int, default=1,
+                    help="1: also measure BASELINE configs[0], [1], [4] and the GEMM drop-in after the timed "
+                         "region (rank 0, N = 1) and report them under extra_configs")
     ap.add_argument("--precision", choices=("int8", "fp8"), default="int8",
                     help="int8 = the headline (configs[2]/[3]); fp8 = e4m3 activations + per-channel "
                          "e4m3 weights on the fp8 MFMA (configs[4])")
@@ -121,6 +125,27 @@ def pmc_traffic(kernel_family):
         return None
 
 
+def host_threads():
+    """CPU threads this process may use: its affinity set, capped by
+    OMP_NUM_THREADS when set (the GPU box gives each one-GPU job a 16-thread
+    share of a larger host and sets OMP_NUM_THREADS=16)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
 def cpu_oracle_baseline(sd, scales, n_images, fp8=False):
     """The oracle (C restatement, 1 thread) on a bounded sample of the same workload."""
     from oracle import oracle as O
@@ -138,21 +163,126 @@ def cpu_oracle_baseline(sd, scales, n_images, fp8=False):
                       f"(single thread), {dt:.2f} s"}
 
 
-def torch_cpu_baseline(sd, n_images):
-    """The reference's 'DeepLearning/ PyTorch fp32 CPU path' counterpart
-    (resnet18_feat.py:95-103 topology) -- reported beside the oracle."""
+def torch_cpu_baseline(sd, batch, iters):
+    """The north star's CPU baseline: the reference's 'DeepLearning/ PyTorch
+    fp32 CPU path' (resnet18_feat.py:95-103 topology, torch.nn) on the host's
+    threads, fp32 inference_mode, one warmup batch then `iters` timed batches."""
     from dlq_amd.models import synthetic_images, torch_resnet18
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     torch.set_num_threads(threads)
     m = torch_resnet18(sd, "cpu")
-    x = synthetic_images(n_images, seed=SEED + 18)
+    x = synthetic_images(batch, seed=SEED + 18)
     with torch.inference_mode():
-        m(x[:2])
-        t0 = time.perf_counter()
         m(x)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            m(x)
         dt = time.perf_counter() - t0
-    return {"value": round(n_images / dt, 3), "unit": "images/s", "cores": threads,
-            "dtype": "f32", "sample": f"{n_images} images, torch {torch.__version__} fp32 inference_mode"}
+    return {"value": round(batch * iters / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "path": "torch-fp32", "dtype": "f32", "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": f"ResNet-18 fp32 (torch {torch.__version__}, inference_mode), batch {batch} x {iters} timed "
+                      f"iterations after 1 warmup batch, {threads} threads, {dt:.2f} s"}
+
+
+def timed_cuda(fn, iters, warmup=3):
+    """ms per call of fn on the current stream (torch events; fn launches there)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def extra_configs(dev):
+    """BASELINE configs[0], [1] and [4] and the exported GEMM, each measured
+    after the headline's timed region (rank 0, N = 1)."""
+    from dlq_amd.models import MLPInt8, MNISTMLP, ResNet18Int8, mlp_weights, mnist_inputs, resnet18_state_dict
+    from dlq_amd.quant import calibrate_mlp, calibrate_resnet18
+    from dlq_amd.models import synthetic_images
+    from dlq_amd.lib import lib, check
+    out = {}
+    # configs[0]: MNIST MLP fp32 on the PyTorch CPU path (v1.py:35-47), B = 1024
+    try:
+        threads = host_threads()
+        torch.set_num_threads(threads)
+        res = {}
+        for hidden in (256, 128):
+            W1, b1, W2, b2 = mlp_weights(hidden=hidden)
+            m = MNISTMLP(W1, b1, W2, b2).eval()
+            x = torch.from_numpy(mnist_inputs(1024))
+            with torch.inference_mode():
+                for _ in range(3):
+                    m(x)
+                t0 = time.perf_counter()
+                n = 0
+                while time.perf_counter() - t0 < 1.0:
+                    m(x)
+                    n += 1
+                dt = time.perf_counter() - t0
+            res[f"784x{hidden}x10"] = {"value": round(1024 * n / dt, 1), "unit": "images/s",
+                                       "ms_per_batch": round(dt * 1e3 / n, 4)}
+        out["configs[0] mnist_mlp_fp32_torch_cpu"] = {"batch": 1024, "threads": threads, "cpu_model": cpu_model(),
+                                                      **res}
+    except Exception as e:  # reported context, never fatal
+        out["configs[0] error"] = repr(e)
+    # configs[1]: MNIST int8 FC GEMMs on the GPU (dlq_mlp_*), B = 1024, 784x128x10
+    try:
+        W1, b1, W2, b2 = mlp_weights(hidden=128)
+        xs = mnist_inputs(1024)
+        s_in, s_h = calibrate_mlp(W1, b1, xs)
+        mlp = MLPInt8(W1, b1, W2, b2, s_in, s_h, max_batch=1024)
+        xd = torch.from_numpy(xs).to(dev)
+        yd = torch.empty((1024, 10), dtype=torch.float32, device=dev)
+        ms = timed_cuda(lambda: mlp.forward(xd, yd), 200)
+        macs = 1024 * (784 * 128 + 128 * 10)
+        out["configs[1] mnist_fc_int8_gpu"] = {
+            "shape": "784x128x10", "batch": 1024, "value": round(1024 / (ms * 1e-3), 1), "unit": "images/s",
+            "us_per_forward": round(ms * 1e3, 2), "tops": round(2 * macs / (ms * 1e-3) / 1e12, 3),
+            "frac_of_int8_peak": round(2 * macs / (ms * 1e-3) / 1e12 / PEAK_I8_TOPS, 5),
+            "note": "0.21 GOP per forward: launch/latency bound (4 launches), not MFMA bound"}
+    except Exception as e:
+        out["configs[1] error"] = repr(e)
+    # the exported sgemm_tiled replacement (dlq_gemm_s8s8s32): int8 GEMM TOPS vs peak
+    try:
+        res = {}
+        for (M, N, K) in ((8192, 8192, 8192), (256, 50176, 2304)):
+            A = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+            Bm = torch.randint(-127, 128, (K, N), dtype=torch.int8, device=dev)
+            Cm = torch.empty((M, N), dtype=torch.int32, device=dev)
+            st = torch.cuda.current_stream().cuda_stream
+            fn = lambda: check(lib.dlq_gemm_s8s8s32(A.data_ptr(), Bm.data_ptr(), Cm.data_ptr(), M, N, K, st),  # noqa: E731
+                               "gemm")
+            ms = timed_cuda(fn, 10)
+            tops = 2.0 * M * N * K / (ms * 1e-3) / 1e12
+            res[f"{M}x{N}x{K}"] = {"ms": round(ms, 4), "tops": round(tops, 1), "frac": round(tops / PEAK_I8_TOPS, 4)}
+            del A, Bm, Cm
+        out["gemm_s8s8s32"] = {"kernel": "gemm_s8s8s32_kernel (gemm.hip)", "peak_tops": round(PEAK_I8_TOPS, 1), **res}
+    except Exception as e:
+        out["gemm error"] = repr(e)
+    # configs[4]: fp8 (e4m3) activations + per-channel e4m3 weights, B = 256
+    try:
+        sd = resnet18_state_dict(SEED)
+        sc8 = calibrate_resnet18(sd, synthetic_images(2, seed=SEED + 1), device="cpu", qmax=448.0)
+        m8 = ResNet18Int8(sd, sc8, max_batch=256, precision="fp8")
+        g = torch.Generator(device=dev).manual_seed(SEED + 2000)
+        x8 = (torch.rand((256, 3, 224, 224), generator=g, device=dev) * 4.0 - 2.0).contiguous()
+        lg = torch.empty((256, 1000), dtype=torch.float32, device=dev)
+        ms = timed_cuda(lambda: m8.forward(x8, lg), 20, warmup=5)
+        c_macs, f_macs = m8.macs_per_image()
+        out["configs[4] resnet18_fp8"] = {
+            "value": round(256 / (ms * 1e-3), 1), "unit": "images/s", "ms_per_forward": round(ms, 4),
+            "tflops": round(2 * (c_macs + f_macs) * 256 / (ms * 1e-3) / 1e12, 1),
+            "frac_of_fp8_peak": round(2 * (c_macs + f_macs) * 256 / (ms * 1e-3) / 1e12 / PEAK_I8_TOPS, 4),
+            "timing": "torch events around 20 forwards after 5 warmup, B = 256, inputs resident"}
+        del m8
+    except Exception as e:
+        out["configs[4] error"] = repr(e)
+    return out
 
 
 def main():
@@ -283,12 +413,14 @@ def main():
     if rank == 0 and world == 1:
         try:
             if args.cpu_baseline_images > 0:
-                out["cpu_baseline"] = cpu_oracle_baseline(sd, scales, args.cpu_baseline_images, fp8)
-            if args.torch_cpu_images > 0:
-                out["cpu_torch_fp32"] = torch_cpu_baseline(sd, args.torch_cpu_images)
-            out["cpu_model"] = platform.processor() or platform.machine()
+                out["cpu_baseline"] = torch_cpu_baseline(sd, args.cpu_baseline_images, args.cpu_baseline_iters)
+            if args.oracle_images > 0:
+                out["cpu_oracle_1thread"] = cpu_oracle_baseline(sd, scales, args.oracle_images, fp8)
+            out["cpu_model"] = cpu_model()
         except Exception as e:  # baseline is reported context, never fatal
             out["cpu_baseline_error"] = repr(e)
+        if args.extras and not fp8:
+            out["extra_configs"] = extra_configs(dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

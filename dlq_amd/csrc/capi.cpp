@@ -15,14 +15,6 @@ namespace dlq {
 
 static thread_local std::string g_err;
 
-int debug_bits() {
-  static const int bits = [] {
-    const char* e = std::getenv("DLQ_DBG");
-    return e ? std::atoi(e) : 0;
-  }();
-  return bits;
-}
-
 void set_error(const std::string& msg) { g_err = msg; }
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -105,12 +97,7 @@ void pack_conv_weights(const int8_t* q, int OC, int IC, int kH, int kW, int C, i
 }
 
 bool wide_layout(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW) {
-  static const bool force_v1 = [] {
-    const char* e = std::getenv("DLQ_CONV_V1");
-    return e && e[0] == '1';
-  }();
-  return !force_v1 && (conv3x3w_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW) ||
-                       conv3x3s2_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW));
+  return conv3x3w_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW) || conv3x3s2_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW);
 }
 
 size_t packed_bytes_for(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW) {
@@ -191,17 +178,6 @@ int dlq_quantize_rows_s8(const float* x, int rows, int cols, int ldy, float inv_
 }
 
 namespace {
-// Stride-1 wide convs: the 392-px item kernel (conv3x3i.hip); DLQ_WIDE_256=1
-// selects the earlier 256-px item kernel (conv3x3w.hip, same weight image)
-// for A/B timing.
-hipError_t launch_wide_s1(const ConvArgs& a, hipStream_t s) {
-  static const bool v256 = [] {
-    const char* e = std::getenv("DLQ_WIDE_256");
-    return e && e[0] == '1';
-  }();
-  return v256 ? launch_conv3x3w(a, s) : launch_conv3x3i(a, s);
-}
-
 // Validation + ConvArgs of one conv launch (shared by the conv entry points).
 int conv_args(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
               const float* beta, const int8_t* residual, float res_scale, int relu, int out_kind, void* y,
@@ -227,7 +203,7 @@ int conv_args(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, c
   a.K = is_stem(d->C, d->kH, d->kW) ? kStemK : d->kH * d->kW * d->C;
   a.kH = d->kH; a.kW = d->kW; a.sH = d->sH; a.sW = d->sW; a.pH = d->pH; a.pW = d->pW;
   a.relu = relu ? 1 : 0; a.out_kind = out_kind;
-  a.dbg = debug_bits();
+  a.dbg = 0;
   if (a.OH <= 0 || a.OW <= 0) return fail(DLQ_ERR_ARG, "conv2d: empty output");
   const long long P = (long long)a.N * a.OH * a.OW;
   const long long in_bytes = (long long)a.N * a.H * a.W * a.C;
@@ -263,8 +239,8 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
   if (rc) return rc;
   if (a.P == 0) return DLQ_OK;
   hipError_t e = !wide ? launch_conv(a, (hipStream_t)stream)
-                 : a.sH == 2 ? launch_conv3x3s2(a, nullptr, nullptr, nullptr, nullptr, (hipStream_t)stream)
-                             : launch_wide_s1(a, (hipStream_t)stream);
+                 : a.sH == 2 ? launch_conv3x3s2i(a, nullptr, nullptr, nullptr, nullptr, (hipStream_t)stream)
+                             : launch_conv3x3i(a, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d launch: ") + hipGetErrorString(e));
 }
 
@@ -289,9 +265,8 @@ int dlq_conv2d_s2_ds_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8
   bool wide = false;
   int rc = conv_args(d, x, w_packed, alpha, beta, nullptr, 0.f, 1, DLQ_OUT_S8, y, a, wide);
   if (rc) return rc;
-  if (!wide) return fail(DLQ_ERR_STATE, "conv2d_s2_ds: disabled by DLQ_CONV_V1");
   if (a.P == 0) return DLQ_OK;
-  hipError_t e = launch_conv3x3s2(a, w_ds, alpha_ds, beta_ds, y_ds, (hipStream_t)stream);
+  hipError_t e = launch_conv3x3s2i(a, w_ds, alpha_ds, beta_ds, y_ds, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d_s2_ds launch: ") + hipGetErrorString(e));
 }
 

@@ -238,7 +238,7 @@ __global__ __launch_bounds__(NWAVE * 64, 1) void conv3x3s1_kernel(ConvArgs a) {
           }
       }
     }
-    if (s + 1 < nstages && !(a.dbg & 2)) issue(s + 1);
+    if (s + 1 < nstages && !DLQ_ABL(a, 2)) issue(s + 1);
 
     const int8_t* pb = lds + (s & 1) * G::PBYTES;
     const int8_t* wb = lds + OFF_W + (G::RESIDENT ? 0 : (s & 1)) * WBYTES;
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(NWAVE * 64, 1) void conv3x3s1_kernel(ConvArgs a) {
         bf[fn] = *(const v4i*)(lds + (((vmask[fn] >> tap) & 1) ? (int)(pb - lds) + off : OFF_Z));
       }
     };
-    if (!(a.dbg & 1)) {
+    if (!DLQ_ABL(a, 1)) {
       v4i af0[2], bf0[FN], af1[2], bf1[FN];
       load_step(0, af0, bf0);
 #pragma unroll
@@ -325,7 +325,7 @@ __global__ __launch_bounds__(NWAVE * 64, 1) void conv3x3s1_kernel(ConvArgs a) {
           const int u = r * 64 + lane, pl = u >> 2, lc = u & 3;
           const v4i v = *(const v4i*)(sb + pl * 64 + ((lc ^ ((pl >> 2) & 3)) << 4));
           const int p = cur.p0 + wave * PXW + pl;
-          const bool keep = p < cur.pend && (!(a.dbg & 4) || v[0] == 0x9e3779b9);
+          const bool keep = p < cur.pend && (!DLQ_ABL(a, 4) || v[0] == 0x9e3779b9);
           v4i* dst = keep ? (v4i*)((int8_t*)a.y + (size_t)p * a.OC + cur.ot * 64 + lc * 16)
                           : (v4i*)(g_trash + lane * 16);
           *dst = v;

@@ -30,7 +30,7 @@
 // Stages (weight block [OT oc][9 taps x 32 B + 16 pad] + the patch of one
 // 32-channel slice) stream through a 2-slot LDS-DMA ring: stage s+1 is issued
 // right after the barrier that opens stage s, one piece per tap between the
-// MFMAs.  Epilogue as in conv3x3w.hip: MFMA-layout requantisation, two
+// MFMAs.  Epilogue: MFMA-layout requantisation, two
 // v_permlane32_swap per tile, one 16-byte store per lane and tile.
 #include <type_traits>
 
@@ -245,7 +245,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       wait_vm_const<STORES>();
     else
       wait_vm_const<0>();
-    if (!(a.dbg & 16)) __builtin_amdgcn_s_barrier();  // dbg 16: timing experiment only (races)
+    __builtin_amdgcn_s_barrier();
     ISTAMP(1 + 2 * s);
     const bool more = s + 1 < nst;
     if (more && loader) prep_for(s + 1);
@@ -255,7 +255,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #pragma unroll
       for (int f = 0; f < NF; ++f) acc[f] = Acc{0};
     }
-    const bool dma = more && loader && !(a.dbg & 2);
+    const bool dma = more && loader && !DLQ_ABL(a, 2);
     const int sb = (s & 1) * G::SLOT;
     const int8_t* abase = lds + sb + a_row;
     // this stage's slot: move the tap base registers by one slot (each tap
@@ -366,7 +366,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     }  // int8 MFMA loop
 
     ISTAMP(2 + 2 * s);
-    if (j != NS - 1 || (a.dbg & 4)) continue;  // dbg 4: timing experiment without the epilogue
+    if (j != NS - 1 || DLQ_ABL(a, 4)) continue;  // probe builds: timing without the epilogue
     // ---- fused epilogue of the item ----
     if constexpr (OUT == 2) {
 #pragma unroll
@@ -517,7 +517,7 @@ hipError_t launch_conv3x3i_f8(const ConvArgs& a, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
-// Same shapes and the same packed weight image as conv3x3w (conv3x3w_pack).
+// Weight image: conv3x3w_pack (wpack.cpp).
 hipError_t launch_conv3x3i(const ConvArgs& a, hipStream_t s) {
   if (a.OCp != a.OC || a.C != a.OC || a.H != a.W) return hipErrorInvalidValue;
   switch (a.W) {

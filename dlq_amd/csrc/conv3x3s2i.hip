@@ -31,7 +31,6 @@
 // slice (tap 8 paired with zeros, 5 MFMAs per slice); the downsample's MFMA
 // takes the pair (tap 4, tap 5) with its A fragment's upper half zero, so only
 // the centre tap contributes.  B pairs stream through a 3-deep register ring.
-#include <cstdlib>
 #include <type_traits>
 
 #include "device_common.h"
@@ -310,7 +309,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
           if (pr == 1) fd2 = cat8(*(const v4i*)(lds + wb + d_row), v4i{0, 0, 0, 0});  // used with pair (4, 5)
         }
         const int k0 = 2 * pr * DPW / 9, k1 = (2 * pr + 2 < 9 ? 2 * pr + 2 : 9) * DPW / 9;
-        if (more && !(a.dbg & 2)) {
+        if (more && !DLQ_ABL(a, 2)) {
 #pragma unroll
           for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
         }
@@ -343,7 +342,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
         if (tap == 3) fd = *(const v4i*)(lds + wb + d_row);  // the downsample's A fragment, used at tap 4
       }
       const int k0 = tap * DPW / 9, k1 = (tap + 1) * DPW / 9;
-      if (more && !(a.dbg & 2)) {  // dbg 2: timing experiment without the DMA
+      if (more && !DLQ_ABL(a, 2)) {  // probe builds: timing without the DMA
 #pragma unroll
         for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
       }
@@ -379,7 +378,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     }
     }  // int8 MFMA loop
 
-    if (j != NS - 1 || (a.dbg & 4)) continue;  // dbg 4: timing experiment without the epilogues
+    if (j != NS - 1 || DLQ_ABL(a, 4)) continue;  // probe builds: timing without the epilogues
     // ---- fused epilogues of the item ----
     if constexpr (OUT == 2) {
 #pragma unroll
@@ -496,11 +495,7 @@ hipError_t launch_j(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, c
                        nullptr);
   } else if (w_ds) {
     if constexpr (OW == 28 && C == 64) {  // layer2.0: one output-channel tile -> resident weights
-      static const bool ring = [] {
-        const char* e = std::getenv("DLQ_S2_RING");
-        return e && e[0] == '1';
-      }();
-      if (a.OCp == JOT && !ring) {
+      if (a.OCp == JOT) {
         hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true, F8, true>), grid, block, 0, s, a, w_ds, al_ds, be_ds,
                            y_ds);
         return hipGetLastError();
@@ -528,8 +523,7 @@ hipError_t launch_s2i(const ConvArgs& a, const int8_t* w_ds, const float* al_ds,
 
 }  // namespace
 
-// Same shapes and packed weight images as conv3x3s2.hip (conv3x3w_pack for
-// conv1, downsample_pack for the 1x1).
+// Weight images: conv3x3w_pack for conv1, downsample_pack for the 1x1 (wpack.cpp).
 hipError_t launch_conv3x3s2i(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, const float* be_ds,
                              int8_t* y_ds, hipStream_t s) {
   return launch_s2i<false>(a, w_ds, al_ds, be_ds, y_ds, s);

@@ -23,11 +23,18 @@ struct ConvArgs {
   int P;     // N*OH*OW
   int relu;
   int out_kind;
-  int dbg;  // ablation bits for timing builds (0 in every real call): 1 skip MFMA, 2 skip DMA, 4 skip stores
+  int dbg;  // ablation bits, read only by DLQ_ABLATION probe builds (tools/probe): 2 skip DMA, 4 skip epilogue
 };
 
-// Ablation bits from the DLQ_DBG environment variable (read once; 0 = off).
-int debug_bits();
+// Timing-ablation switches exist only in probe builds (tools/probe/*.hip
+// define DLQ_ABLATION before including a kernel source); in libdlq.so every
+// DLQ_ABL() is the constant false, so no input can make a shipped kernel skip
+// work or a barrier.
+#ifdef DLQ_ABLATION
+#define DLQ_ABL(a, bit) (((a).dbg & (bit)) != 0)
+#else
+#define DLQ_ABL(a, bit) false
+#endif
 
 // Stem packing: C == 4, 7x7 taps padded to 8x8 -> K = 256.
 constexpr int kStemC = 4;
@@ -40,21 +47,18 @@ bool is_stem(int C, int kH, int kW);
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s);
 bool conv3x3s1_supported(const ConvArgs& a);
 hipError_t launch_conv3x3s1(const ConvArgs& a, hipStream_t s);
-// Wide stride-1 3x3 convs (conv3x3w.hip): own weight layout, selected by shape.
+// Wide stride-1 3x3 convs: the shapes, the weight image (wpack.cpp) and the
+// 392-px item kernel (conv3x3i.hip).
 bool conv3x3w_shape(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW);
 size_t conv3x3w_packed_bytes(int OC, int C);
 void conv3x3w_pack(const int8_t* q_oihw, int OC, int IC, int C, int8_t* out);
-hipError_t launch_conv3x3w(const ConvArgs& a, hipStream_t s);
-// Same shapes and weight image, 392-px items (conv3x3i.hip).
 hipError_t launch_conv3x3i(const ConvArgs& a, hipStream_t s);
-// Stride-2 3x3 convs (conv3x3s2.hip), wide weight layout, optional fused 1x1/s2
-// downsample (w_ds == nullptr: conv only).
+// Stride-2 3x3 convs: the shapes and the 1x1/s2 downsample image (wpack.cpp),
+// conv1 in the wide image, and the 196-px item kernel (conv3x3s2i.hip) with
+// the optional fused downsample (w_ds == nullptr: conv only).
 bool conv3x3s2_shape(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW);
 size_t downsample_packed_bytes(int OC, int C);
 void downsample_pack(const int8_t* q_oc_ic, int OC, int IC, int C, int8_t* out);
-hipError_t launch_conv3x3s2(const ConvArgs& a, const int8_t* w_ds, const float* alpha_ds, const float* beta_ds,
-                            int8_t* y_ds, hipStream_t s);
-// Same shapes and weight images, 196-px items (conv3x3s2i.hip).
 hipError_t launch_conv3x3s2i(const ConvArgs& a, const int8_t* w_ds, const float* alpha_ds, const float* beta_ds,
                              int8_t* y_ds, hipStream_t s);
 // Fused layer1 basic block (block_l1.hip): C == OC == 64 at 56x56, identity
@@ -80,6 +84,8 @@ hipError_t launch_linear(const int8_t* x, int N, int K, const int8_t* w, int OC,
                          const float* beta, int relu, int out_kind, void* y, hipStream_t s);
 hipError_t launch_gap_fc(const int8_t* x, int N, int C, int HW, float k, const int8_t* w, int OC,
                          const float* alpha, const float* beta, float* y, hipStream_t s);  // C == 512, HW <= 56
+// dlq_gemm_s8s8s32 (gemm.hip): row-major int8 A[M][K] . B[K][N] -> int32 C.
+hipError_t launch_gemm_s8s8s32(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, hipStream_t s);
 hipError_t launch_im2col_nchw(const int8_t* x, int N, int C, int H, int W, int kH, int kW, int sH,
                               int sW, int pH, int pW, int8_t* col, hipStream_t s);
 
@@ -100,6 +106,18 @@ void pack_conv_weights_f8(int C, int OC, int H, int W, int kH, int kW, int sH, i
 uint8_t f8_encode_host(float y);
 uint8_t f8_requant_host(float y, float lo);
 void quantize_weights_f8(const float* w, int OC, int K, uint8_t* q, float* scale);
+
+// Reference-semantics fp32 ops (ref_f32.hip; oracle.c ora_*_f32 bit for bit),
+// NCHW over B images.  amax (nullable): device uint, max |output| as float bits.
+hipError_t launch_ref_conv_bn(const float* x, int B, int IC, int H, int W, const float* w, int OC, int k, int s, int p,
+                              const float* g, const float* b, const float* m, const float* d, int relu, float* y,
+                              unsigned* amax, hipStream_t st);
+hipError_t launch_ref_add_relu(float* y, const float* skip, long n, unsigned* amax, hipStream_t st);
+hipError_t launch_ref_maxpool(const float* x, int NC, int H, int W, float* y, hipStream_t st);
+hipError_t launch_ref_gap(const float* x, int NC, int HW, float* y, unsigned* amax, hipStream_t st);
+hipError_t launch_ref_fc(const float* g, int B, const float* W, const float* bias, int O, int I, float* out,
+                         hipStream_t st);
+hipError_t launch_amax(const float* x, long n, unsigned* amax, hipStream_t st);
 
 // Thread-local error message (capi.cpp).
 void set_error(const std::string& msg);

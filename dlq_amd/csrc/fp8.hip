@@ -288,12 +288,9 @@ uint8_t f8_requant_host(float y, float lo) {
   return f8_encode_host(y + 0.0f);
 }
 
-// DLQ_F8_GENERIC=1 (read at every call: a test switch) keeps every fp8 conv
-// on the generic kernel and layout.
+// The wide kernels' shapes take their image; every other fp8 conv the generic one.
 bool f8_wide(int C, int OC, int H, int W, int kH, int kW, int sH, int sW, int pH, int pW) {
-  const char* e = std::getenv("DLQ_F8_GENERIC");
-  return !(e && e[0] == '1') && (conv3x3w_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW) ||
-                                 conv3x3s2_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW));
+  return conv3x3w_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW) || conv3x3s2_shape(C, OC, H, W, kH, kW, sH, sW, pH, pW);
 }
 
 namespace {

@@ -469,11 +469,7 @@ int packed_oc(int OC) { return OC <= 64 ? 64 : (OC + 127) / 128 * 128; }
 bool is_stem(int C, int kH, int kW) { return C == kStemC && kH == 7 && kW == 7; }
 
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {
-  static const bool force_v1 = [] {
-    const char* e = std::getenv("DLQ_CONV_V1");
-    return e && e[0] == '1';
-  }();
-  if (!force_v1 && conv3x3s1_supported(a)) return launch_conv3x3s1(a, s);
+  if (conv3x3s1_supported(a)) return launch_conv3x3s1(a, s);
   if (is_stem(a.C, a.kH, a.kW)) return launch_cfg<64, 256, 1, 1>(a, s);
   if (a.OCp == 64) return launch_cfg<64, 256, 1, 0>(a, s);
   return launch_cfg<128, 128, 2, 0>(a, s);

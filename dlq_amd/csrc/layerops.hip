@@ -32,40 +32,6 @@ __global__ void quantize_f32_s8_kernel(const float* __restrict__ x, size_t n, fl
     q[i] = (int8_t)sat_rne(x[i] * inv_s);
 }
 
-// C[M][N] = A[M][K] . B[K][N] (row-major; sgemm_tiled.cu:5-46 layout), int32.
-// One wave per 32x32 tile, v_mfma_i32_32x32x32_i8; fragments gathered with
-// bounds checks (any M, N, K).
-__global__ __launch_bounds__(64) void gemm_s8s8s32_kernel(const int8_t* __restrict__ A, const int8_t* __restrict__ B,
-                                                          int32_t* __restrict__ C, int M, int N, int K) {
-  const int lane = threadIdx.x, lr = lane & 31, lh = lane >> 5;
-  const int m = blockIdx.y * 32 + lr, n = blockIdx.x * 32 + lr;
-  v16i acc = v16i{0};
-  for (int k0 = 0; k0 < K; k0 += 32) {
-    v4i a, b;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      unsigned ua = 0, ub = 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = k0 + lh * 16 + w * 4 + e;
-        const unsigned va = (m < M && k < K) ? (unsigned)(uint8_t)A[(size_t)m * K + k] : 0u;
-        const unsigned vb = (n < N && k < K) ? (unsigned)(uint8_t)B[(size_t)k * N + n] : 0u;
-        ua |= va << (8 * e);
-        ub |= vb << (8 * e);
-      }
-      a[w] = (int)ua;
-      b[w] = (int)ub;
-    }
-    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);  // D[m][n]
-  }
-  // D reg r, lane (lr, lh): row m0 + (r&3) + 8(r>>2) + 4lh, column n0 + lr
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int mm = blockIdx.y * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh, nn = blockIdx.x * 32 + lr;
-    if (mm < M && nn < N) C[(size_t)mm * N + nn] = acc[r];
-  }
-}
-
 template <typename T>
 __global__ void nchw_to_nhwc_kernel(const T* __restrict__ x, int N, int C, int HW, int Cs, T* __restrict__ y) {
   const size_t total = (size_t)N * HW * Cs;
@@ -194,9 +160,9 @@ int dlq_gemm_s8s8s32(const int8_t* A, const int8_t* B, int32_t* C, int M, int N,
   if (M < 0 || N < 0 || K < 0) return fail(DLQ_ERR_ARG, "gemm_s8s8s32: negative size");
   if (M == 0 || N == 0) return DLQ_OK;
   if (!A || !B || !C) return fail(DLQ_ERR_ARG, "gemm_s8s8s32: null pointer");
-  hipLaunchKernelGGL(gemm_s8s8s32_kernel, dim3((N + 31) / 32, (M + 31) / 32), dim3(64), 0, (hipStream_t)stream, A,
-                     B, C, M, N, K);
-  return status(launched(), "gemm_s8s8s32");
+  if ((long long)M * K >= (1LL << 31) || (long long)K * N >= (1LL << 31) || (long long)M * N >= (1LL << 31))
+    return fail(DLQ_ERR_ARG, "gemm_s8s8s32: operand exceeds 2^31 elements");
+  return status(launch_gemm_s8s8s32(A, B, C, M, N, K, (hipStream_t)stream), "gemm_s8s8s32");
 }
 
 size_t dlq_conv2d_nchw_workspace_bytes(int N, int IC, int H, int W, int OC, int kH, int kW, int sH, int sW, int pH,

@@ -75,8 +75,6 @@ struct dlq_resnet18 {
   float* fc_beta = nullptr;
   // workspace
   int max_batch = 0;
-  int8_t* xq = nullptr;       // [B][224][224][4]
-  int8_t* c1 = nullptr;       // [B][112][112][64]
   int8_t* buf[4] = {};        // block activations, each B*56*56*64 bytes
   int8_t* gq = nullptr;       // [B][512]
   std::vector<void*> allocs;
@@ -112,6 +110,9 @@ struct dlq_resnet18 {
   const float* g_x = nullptr;
   float* g_logits = nullptr;
   int g_B = 0;
+  // stage outputs of the last reference-semantics fp32 forward
+  // (dlq_resnet18_forward_f32): fp32 NCHW device buffers owned here
+  std::map<std::string, std::pair<float*, size_t>> stage_f32;
 };
 
 namespace {
@@ -208,7 +209,7 @@ void free_all(dlq_resnet18* m) {
   m->allocs.clear();
   for (auto& c : m->convs) { c.w = nullptr; c.wf = nullptr; c.alpha = nullptr; c.beta = nullptr; }
   m->fc_w = nullptr; m->fc_alpha = m->fc_beta = nullptr;
-  m->xq = m->c1 = m->gq = m->stem_w = nullptr;
+  m->gq = m->stem_w = nullptr;
   m->stem_alpha = nullptr;
   for (auto& b : m->buf) b = nullptr;
   m->keepbuf.clear();
@@ -216,16 +217,6 @@ void free_all(dlq_resnet18* m) {
 }
 
 float inv_scale(float s) { return 1.0f / s; }
-
-// DLQ_STEM_UNFUSED=1 runs quantise / conv1 / maxpool as three launches
-// (A/B timing, and exposes the "input_q" and "conv1" stages).
-bool unfused_stem() {
-  static const bool v = [] {
-    const char* e = std::getenv("DLQ_STEM_UNFUSED");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
 
 // DLQ_HEAD_SPLIT=1 (read at every call): GAP and FC as two launches
 // (gap16_kernel + linear_kernel) instead of the fused gap_fc_kernel.
@@ -272,14 +263,10 @@ int conv_family(const ConvLayer& c, int H) {
   return DLQ_FAM_OTHER;
 }
 
-// The layer1 block runs as one fused launch (DLQ_BLOCK_UNFUSED=1: two conv
-// launches, for A/B timing).
+// The layer1 blocks (64 -> 64 channels at 56x56, identity skip) run as one
+// fused launch each (block_l1.hip).
 bool fused_l1_block(const dlq_resnet18* m, const Block& b, int H, int W) {
-  static const bool off = [] {
-    const char* e = std::getenv("DLQ_BLOCK_UNFUSED");
-    return e && e[0] == '1';
-  }();
-  if (off || b.down) return false;
+  if (b.down) return false;
   const ConvLayer& c1 = m->convs[b.c1];
   const ConvLayer& c2 = m->convs[b.c2];
   return c1.k == 3 && c1.s == 1 && c1.p == 1 && c2.k == 3 && c2.s == 1 && c2.p == 1 &&
@@ -466,6 +453,7 @@ void dlq_resnet18_destroy(dlq_resnet18* m) {
   for (hipEvent_t e : m->ev) (void)hipEventDestroy(e);
   if (m->gexec) (void)hipDeviceSynchronize();  // a replay may still be in flight
   free_all(m);
+  for (auto& kv : m->stage_f32) (void)hipFree(kv.second.first);
   if (m->gs) (void)hipStreamDestroy(m->gs);
   delete m;
 }
@@ -587,7 +575,11 @@ int dlq_resnet18_save_manifest(const dlq_resnet18* m, const char* dir, int int8)
   }
   js << "\n  }\n}\n";
   const std::string j = js.str();
-  return write_file(std::string(dir) + "/manifest.json", j.data(), j.size());
+  int rc = write_file(std::string(dir) + "/manifest.json", j.data(), j.size());
+  // the activation scales travel with the weights: the launcher reads
+  // <dir>/scales.txt when --scales is not given
+  if (!rc && !m->scales.empty()) rc = dlq_resnet18_save_scales(m, (std::string(dir) + "/scales.txt").c_str());
+  return rc;
 }
 
 int dlq_resnet18_save_scales(const dlq_resnet18* m, const char* path) {
@@ -630,7 +622,7 @@ int upload(dlq_resnet18* m, T** dst, const void* src, size_t bytes) {
 
 // fp8 prepare: e4m3 per-channel weights in the generic packed layout, BN
 // folded exactly as the int8 path (fold_bn with the e4m3 weight scales),
-// FC row-major; workspace includes the unfused stem's buffers.
+// FC row-major.
 int prepare_f8(dlq_resnet18* m, int max_batch) {
   int rc;
   for (auto& c : m->convs) {
@@ -680,9 +672,6 @@ int prepare_f8(dlq_resnet18* m, int max_batch) {
   }
   const size_t B = (size_t)max_batch;
   if ((rc = dev_alloc(m, &m->gq, B * 512))) return rc;
-  if (unfused_stem() &&
-      ((rc = dev_alloc(m, &m->xq, B * 224 * 224 * kStemC)) || (rc = dev_alloc(m, &m->c1, B * 112 * 112 * 64))))
-    return rc;
   for (auto& b : m->buf)
     if ((rc = dev_alloc(m, &b, B * 56 * 56 * 64))) return rc;
   if (m->keep) {
@@ -788,9 +777,6 @@ int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
   // Workspace (int8 NHWC), sized once for max_batch.
   const size_t B = (size_t)max_batch;
   if ((rc = dev_alloc(m, &m->gq, B * 512))) return rc;
-  if (unfused_stem() &&
-      ((rc = dev_alloc(m, &m->xq, B * 224 * 224 * kStemC)) || (rc = dev_alloc(m, &m->c1, B * 112 * 112 * 64))))
-    return rc;
   for (auto& b : m->buf)
     if ((rc = dev_alloc(m, &b, B * 56 * 56 * 64))) return rc;
   if (m->keep) {
@@ -851,23 +837,10 @@ int forward_pass_f8(dlq_resnet18* m, const float* x, int B, float* logits, hipSt
   const ConvLayer& st = m->convs[m->stem];
   int ci = 0;
   int8_t* cur = m->buf[ci];
-  if (!unfused_stem()) {
-    if ((rc = mark(m, s, DLQ_FAM_STEM))) return rc;
-    rc = dlq_stem_fused_f8(x, B, (const uint8_t*)m->stem_w, m->stem_alpha, st.beta, inv_scale(m->scales.at("input")),
-                           (uint8_t*)cur, s);
-    if (rc) return rc;
-  } else {
-    if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
-    rc = dlq_quantize_nchw_to_nhwc_f8(x, B, 3, 224, 224, kStemC, inv_scale(m->scales.at("input")), (uint8_t*)m->xq,
-                                      s);
-    if (rc) return rc;
-    if (record) m->stage["input_q"] = {m->xq, nB * 224 * 224 * kStemC};
-    if ((rc = conv_f8(m, st, m->xq, B, 224, nullptr, 0.f, true, m->c1, s))) return rc;
-    if (record) m->stage["conv1"] = {m->c1, nB * 112 * 112 * 64};
-    if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
-    // post-ReLU e4m3 codes are 0x00..0x7e: their int8 max is the value max
-    if ((rc = dlq_maxpool2d_3x3_s2p1_nhwc_s8(m->c1, B, 64, 112, 112, cur, s))) return rc;
-  }
+  if ((rc = mark(m, s, DLQ_FAM_STEM))) return rc;
+  rc = dlq_stem_fused_f8(x, B, (const uint8_t*)m->stem_w, m->stem_alpha, st.beta, inv_scale(m->scales.at("input")),
+                         (uint8_t*)cur, s);
+  if (rc) return rc;
   if (record && (rc = record_stage(m, "stem_pool", cur, nB * 56 * 56 * 64, s))) return rc;
   int H = 56;
   for (const Block& b : m->blocks) {
@@ -942,27 +915,11 @@ int forward_pass(dlq_resnet18* m, const float* x, int B, float* logits, hipStrea
   int8_t* cur = bufp(ci);
   int8_t* gq = m->gq + img0 * 512;
   const ConvLayer& st = m->convs[m->stem];
-  if (!unfused_stem()) {
-    // 0+1) fused stem: quantise + conv 7x7/s2 + BN + ReLU + maxpool 3x3/s2
-    //      (infer_e2e.cu:255-293) in one launch
-    if ((rc = mark(m, s, DLQ_FAM_STEM))) return rc;
-    rc = dlq_stem_fused_s8(x, B, m->stem_w, m->stem_alpha, st.beta, inv_scale(m->scales.at("input")), cur, stream);
-    if (rc) return rc;
-  } else {
-    // unfused reference sequence (A/B and parity of the fused kernel)
-    if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
-    rc = dlq_quantize_nchw_to_nhwc_s8(x, B, 3, 224, 224, kStemC, inv_scale(m->scales.at("input")), m->xq, stream);
-    if (rc) return rc;
-    if (record) m->stage["input_q"] = {m->xq, nB * 224 * 224 * kStemC};
-    int CH, CW;
-    if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
-    rc = conv2d_nhwc_s8(m, st, m->xq, B, 224, 224, nullptr, 0.f, true, m->c1, s, &CH, &CW);
-    if (rc) return rc;
-    if (record) m->stage["conv1"] = {m->c1, nB * CH * CW * 64};
-    if ((rc = mark(m, s, DLQ_FAM_OTHER))) return rc;
-    rc = dlq_maxpool2d_3x3_s2p1_nhwc_s8(m->c1, B, 64, CH, CW, cur, stream);
-    if (rc) return rc;
-  }
+  // 0+1) fused stem: quantise + conv 7x7/s2 + BN + ReLU + maxpool 3x3/s2
+  //      (infer_e2e.cu:255-293) in one launch
+  if ((rc = mark(m, s, DLQ_FAM_STEM))) return rc;
+  rc = dlq_stem_fused_s8(x, B, m->stem_w, m->stem_alpha, st.beta, inv_scale(m->scales.at("input")), cur, stream);
+  if (rc) return rc;
   if (record && (rc = record_stage(m, "stem_pool", cur, nB * H * W * 64, s))) return rc;
   // 2-5) layer1..layer4 (:300-415)
   for (size_t bi = 0; bi < m->blocks.size(); ++bi) {
@@ -1164,7 +1121,7 @@ int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes)
         bytes[DLQ_FAM_S2DS] += (k == 1 ? (double)c.H * c.H * c.Cstore : 0.0) + (double)OH * OH * c.OC;
         continue;
       }
-      if (&c == &m->convs[m->stem] && !unfused_stem()) {  // fp32 input read + pooled e4m3 output
+      if (&c == &m->convs[m->stem]) {  // fp32 input read + pooled e4m3 output
         macs[DLQ_FAM_STEM] = (double)c.OC * c.IC * c.k * c.k * OH * OH;
         bytes[DLQ_FAM_STEM] = 3.0 * 224 * 224 * 4 + 56.0 * 56 * 64;
         continue;
@@ -1236,6 +1193,216 @@ int dlq_resnet18_stage(dlq_resnet18* m, const char* name, void* dst, size_t cap,
   hipError_t e = hipMemcpyAsync(dst, it->second.first, it->second.second, hipMemcpyDeviceToDevice,
                                 (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : hip_fail(e, "stage copy");
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Reference-semantics fp32 forward (ref_f32.hip): infer_e2e.cu:259-438 op for
+// op on the GPU, for activation-scale calibration and the launcher's --fp32
+// mode.  Model preparation / parity, not the timed path: fp32 weights are
+// uploaded per call (as the reference does, :262, :304-334) and freed after.
+namespace {
+
+struct DevArena {  // per-call device allocations, freed on scope exit
+  std::vector<void*> p;
+  ~DevArena() {
+    for (void* q : p) (void)hipFree(q);
+  }
+  template <typename T>
+  int alloc(T** out, size_t bytes) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, bytes ? bytes : 16);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc (fp32 forward)");
+    p.push_back(q);
+    *out = (T*)q;
+    return DLQ_OK;
+  }
+  template <typename T>
+  int upload(T** out, const T* src, size_t n, hipStream_t s) {
+    int rc = alloc(out, n * sizeof(T));
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(*out, src, n * sizeof(T), hipMemcpyHostToDevice, s);
+    return e == hipSuccess ? DLQ_OK : hip_fail(e, "fp32 weight upload");
+  }
+};
+
+int check_tensors(const dlq_resnet18* m) {
+  for (const auto& n : required_tensors(m))
+    if (!m->tensors.count(n) && !m->qtensors.count(n)) return fail(DLQ_ERR_STATE, "missing tensor: " + n);
+  return DLQ_OK;
+}
+
+// Sites in calibration order (dlq_amd/quant.py calibrate_resnet18).
+std::vector<std::string> calib_sites(const dlq_resnet18* m) {
+  std::vector<std::string> s = {"input", "conv1"};
+  for (const Block& b : m->blocks) {
+    s.push_back(b.name + ".conv1");
+    if (b.down) s.push_back(b.name + ".downsample");
+    s.push_back(b.name + ".conv2");
+  }
+  s.push_back("gap");
+  return s;
+}
+
+int keep_f32(dlq_resnet18* m, const char* name, const float* src, size_t n, hipStream_t s) {
+  auto it = m->stage_f32.find(name);
+  if (it != m->stage_f32.end() && it->second.second != n * 4) {
+    (void)hipFree(it->second.first);
+    m->stage_f32.erase(it);
+    it = m->stage_f32.end();
+  }
+  if (it == m->stage_f32.end()) {
+    float* q = nullptr;
+    hipError_t e = hipMalloc(&q, n * 4);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc (fp32 stage)");
+    it = m->stage_f32.emplace(name, std::make_pair(q, n * 4)).first;
+  }
+  hipError_t e = hipMemcpyAsync(it->second.first, src, n * 4, hipMemcpyDeviceToDevice, s);
+  return e == hipSuccess ? DLQ_OK : hip_fail(e, "fp32 stage copy");
+}
+
+// amax (host, per calib_sites order) may be null; logits may be null.
+int ref_forward_f32(dlq_resnet18* m, const float* x, int B, float* logits, std::vector<float>* amax_out,
+                    hipStream_t s) {
+  int rc;
+  if ((rc = check_tensors(m))) return rc;
+  const std::vector<std::string> sites = calib_sites(m);
+  auto site_ix = [&](const std::string& n) {
+    for (size_t i = 0; i < sites.size(); ++i)
+      if (sites[i] == n) return (int)i;
+    return -1;
+  };
+  DevArena ar;
+  unsigned* amax = nullptr;
+  if ((rc = ar.alloc(&amax, sites.size() * 4))) return rc;
+  hipError_t e = hipMemsetAsync(amax, 0, sites.size() * 4, s);
+  if (e != hipSuccess) return hip_fail(e, "amax reset");
+  // conv + BN parameters of one ConvLayer, uploaded
+  struct DevConv {
+    float *w, *g, *b, *mu, *d;
+  };
+  auto upload_conv = [&](const ConvLayer& c, DevConv& dc) {
+    const int K = c.IC * c.k * c.k;
+    const std::vector<float> w = weights_f32(m, c.wname, c.OC, K);
+    std::vector<float> d(c.OC);
+    const std::vector<float>& var = m->tensors.at(c.bn + ".running_var");
+    for (int o = 0; o < c.OC; ++o) d[o] = std::sqrt(var[o] + 1e-5f);  // bn_inference.cu:22 (sqrtf(v + eps))
+    int r;
+    if ((r = ar.upload(&dc.w, w.data(), w.size(), s)) ||
+        (r = ar.upload(&dc.g, m->tensors.at(c.bn + ".weight").data(), (size_t)c.OC, s)) ||
+        (r = ar.upload(&dc.b, m->tensors.at(c.bn + ".bias").data(), (size_t)c.OC, s)) ||
+        (r = ar.upload(&dc.mu, m->tensors.at(c.bn + ".running_mean").data(), (size_t)c.OC, s)) ||
+        (r = ar.upload(&dc.d, d.data(), d.size(), s)))
+      return r;
+    return (int)DLQ_OK;
+  };
+  auto conv = [&](const ConvLayer& c, const float* in, int H, float* out, bool relu, const std::string& site) {
+    DevConv dc;
+    int r = upload_conv(c, dc);
+    if (r) return r;
+    const int ix = site.empty() ? -1 : site_ix(site);
+    hipError_t he = launch_ref_conv_bn(in, B, c.IC, H, H, dc.w, c.OC, c.k, c.s, c.p, dc.g, dc.b, dc.mu, dc.d,
+                                       relu ? 1 : 0, out, ix < 0 ? nullptr : amax + ix, s);
+    return he == hipSuccess ? (int)DLQ_OK : hip_fail(he, "fp32 conv launch");
+  };
+  const size_t nB = (size_t)B;
+  if ((e = launch_amax(x, (long)(nB * 3 * 224 * 224), amax + site_ix("input"), s)) != hipSuccess)
+    return hip_fail(e, "amax launch");
+  float *c1, *buf[4];
+  if ((rc = ar.alloc(&c1, nB * 64 * 112 * 112 * 4))) return rc;
+  for (auto& b : buf)
+    if ((rc = ar.alloc(&b, nB * 64 * 56 * 56 * 4))) return rc;
+  // stem: conv1 -> bn1 -> relu -> maxpool (:255-293)
+  if ((rc = conv(m->convs[m->stem], x, 224, c1, true, "conv1"))) return rc;
+  if ((e = launch_ref_maxpool(c1, B * 64, 112, 112, buf[0], s)) != hipSuccess) return hip_fail(e, "maxpool launch");
+  if ((rc = keep_f32(m, "stem_pool", buf[0], nB * 64 * 56 * 56, s))) return rc;
+  int ci = 0, H = 56;
+  for (const Block& b : m->blocks) {  // basic_block_forward (:156-203)
+    int fi[3], k = 0;
+    for (int i = 0; i < 4; ++i)
+      if (i != ci && k < 3) fi[k++] = i;
+    float *in = buf[ci], *h = buf[fi[0]], *dsb = buf[fi[1]], *out = buf[fi[2]];
+    const ConvLayer& c1l = m->convs[b.c1];
+    const ConvLayer& c2l = m->convs[b.c2];
+    const int OH = out_dim(H, 3, c1l.s, 1);
+    if ((rc = conv(c1l, in, H, h, true, b.name + ".conv1"))) return rc;
+    if ((rc = conv(c2l, h, OH, out, false, ""))) return rc;
+    const float* skip = in;
+    if (b.down) {
+      if ((rc = conv(m->convs[b.ds], in, H, dsb, false, b.name + ".downsample"))) return rc;
+      skip = dsb;
+    }
+    const long n = (long)nB * b.oc * OH * OH;
+    if ((e = launch_ref_add_relu(out, skip, n, amax + site_ix(b.name + ".conv2"), s)) != hipSuccess)
+      return hip_fail(e, "add_relu launch");
+    ci = fi[2];
+    H = OH;
+    if (b.name.size() == 8 && b.name[7] == '1')
+      if ((rc = keep_f32(m, b.name.substr(0, 6).c_str(), out, (size_t)n, s))) return rc;
+  }
+  float *gap, *fw, *fb, *lg;
+  if ((rc = ar.alloc(&gap, nB * 512 * 4)) || (rc = ar.alloc(&lg, nB * 1000 * 4))) return rc;
+  if ((e = launch_ref_gap(buf[ci], B * 512, H * H, gap, amax + site_ix("gap"), s)) != hipSuccess)
+    return hip_fail(e, "gap launch");
+  if ((rc = keep_f32(m, "gap", gap, nB * 512, s))) return rc;
+  const std::vector<float> fcw = weights_f32(m, "fc.weight", 1000, 512);
+  if ((rc = ar.upload(&fw, fcw.data(), fcw.size(), s)) ||
+      (rc = ar.upload(&fb, m->tensors.at("fc.bias").data(), (size_t)1000, s)))
+    return rc;
+  if ((e = launch_ref_fc(gap, B, fw, fb, 1000, 512, lg, s)) != hipSuccess) return hip_fail(e, "fc launch");
+  if ((rc = keep_f32(m, "logits", lg, nB * 1000, s))) return rc;
+  if (logits && (e = hipMemcpyAsync(logits, lg, nB * 4000, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+    return hip_fail(e, "logits copy");
+  std::vector<unsigned> am(sites.size());
+  if ((e = hipMemcpyAsync(am.data(), amax, am.size() * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipStreamSynchronize(s)) != hipSuccess)  // the arena is freed on return
+    return hip_fail(e, "fp32 forward sync");
+  if (amax_out) {
+    amax_out->resize(am.size());
+    for (size_t i = 0; i < am.size(); ++i) {
+      float f;
+      std::memcpy(&f, &am[i], 4);
+      (*amax_out)[i] = f;
+    }
+  }
+  return DLQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dlq_resnet18_forward_f32(dlq_resnet18* m, const float* x, int B, float* logits, void* stream) {
+  if (!m || B < 0) return fail(DLQ_ERR_ARG, "forward_f32: bad args");
+  if (B == 0) return DLQ_OK;
+  if (!x) return fail(DLQ_ERR_ARG, "forward_f32: null input");
+  return ref_forward_f32(m, x, B, logits, nullptr, (hipStream_t)stream);
+}
+
+int dlq_resnet18_calibrate(dlq_resnet18* m, const float* x, int B, float qmax, void* stream) {
+  if (!m || B <= 0 || !x || !(qmax > 0.f)) return fail(DLQ_ERR_ARG, "calibrate: bad args");
+  std::vector<float> amax;
+  int rc = ref_forward_f32(m, x, B, nullptr, &amax, (hipStream_t)stream);
+  if (rc) return rc;
+  const std::vector<std::string> sites = calib_sites(m);
+  for (size_t i = 0; i < sites.size(); ++i) {
+    // dlq_amd/quant.py: float32(max(amax, 1e-8) / qmax), the quotient in double
+    const double a = (double)amax[i] > 1e-8 ? (double)amax[i] : 1e-8;
+    if ((rc = dlq_resnet18_set_scale(m, sites[i].c_str(), (float)(a / (double)qmax)))) return rc;
+  }
+  return DLQ_OK;
+}
+
+int dlq_resnet18_stage_f32(dlq_resnet18* m, const char* name, void* dst, size_t cap, size_t* bytes, void* stream) {
+  if (!m || !name) return fail(DLQ_ERR_ARG, "stage_f32: null argument");
+  auto it = m->stage_f32.find(name);
+  if (it == m->stage_f32.end()) return fail(DLQ_ERR_STATE, std::string("stage_f32: not available: ") + name);
+  if (bytes) *bytes = it->second.second;
+  if (!dst) return DLQ_OK;
+  if (cap < it->second.second) return fail(DLQ_ERR_ARG, "stage_f32: destination too small");
+  hipError_t e = hipMemcpyAsync(dst, it->second.first, it->second.second, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : hip_fail(e, "stage_f32 copy");
 }
 
 int dlq_resnet18_macs_per_image(const dlq_resnet18* m, double* conv_macs, double* fc_macs) {

@@ -88,6 +88,9 @@ _SIGS = {
     "dlq_resnet18_timing": ([_vp, _vp, _vp, C.POINTER(_i)], _i),
     "dlq_resnet18_family_work": ([_vp, _vp, _vp], _i),
     "dlq_resnet18_macs_per_image": ([_vp, C.POINTER(C.c_double), C.POINTER(C.c_double)], _i),
+    "dlq_resnet18_forward_f32": ([_vp, _vp, _i, _vp, _vp], _i),
+    "dlq_resnet18_stage_f32": ([_vp, C.c_char_p, _vp, _sz, C.POINTER(_sz), _vp], _i),
+    "dlq_resnet18_calibrate": ([_vp, _vp, _i, _f, _vp], _i),
     "dlq_mlp_create": ([_i, _i, _i, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, C.POINTER(_vp)], _i),
     "dlq_mlp_destroy": ([_vp], None),
     "dlq_mlp_forward": ([_vp, _vp, _i, _vp, _vp], _i),

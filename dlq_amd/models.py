@@ -141,7 +141,7 @@ def torch_resnet18(sd: dict[str, np.ndarray], device="cpu") -> TorchResNet18:
 
 class ResNet18Int8:
     """dlq_resnet18 engine (C ABI): weights quantised/folded/resident once,
-    forward = 22 launches on the current stream, no host sync."""
+    forward = 16 launches on the current stream (stem, 2 fused layer1 blocks, 3 stride-2 + downsample, 9 wide convs, fused GAP+FC), no host sync."""
 
     def __init__(self, sd: dict[str, np.ndarray], scales: dict[str, float], max_batch: int,
                  keep_stages: bool = False, precision: str = "int8"):
@@ -184,6 +184,39 @@ class ResNet18Int8:
         self._check(self._lib.dlq_resnet18_stage(self.h, name.encode(), t.data_ptr(), t.numel(), C.byref(nb),
                                                  stream_handle()), "stage")
         return t.view(*shape)
+
+    def forward_f32(self, x: torch.Tensor) -> torch.Tensor:
+        """The reference's fp32 forward op for op on the GPU
+        (dlq_resnet18_forward_f32): logits [B,1000] fp32."""
+        from .lib import stream_handle
+        if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.shape[1:] == (3, 224, 224)):
+            raise TypeError("x must be a contiguous CUDA fp32 [B,3,224,224] tensor")
+        out = torch.empty((x.shape[0], 1000), dtype=torch.float32, device=x.device)
+        self._check(self._lib.dlq_resnet18_forward_f32(self.h, x.data_ptr(), x.shape[0], out.data_ptr(),
+                                                       stream_handle()), "resnet18_forward_f32")
+        return out
+
+    def stage_f32(self, name: str) -> torch.Tensor:
+        """fp32 NCHW stage of the last forward_f32 (flat)."""
+        nb = C.c_size_t()
+        self._check(self._lib.dlq_resnet18_stage_f32(self.h, name.encode(), None, 0, C.byref(nb), None), "stage_f32")
+        t = torch.empty(int(nb.value) // 4, dtype=torch.float32, device="cuda")
+        self._check(self._lib.dlq_resnet18_stage_f32(self.h, name.encode(), t.data_ptr(), int(nb.value), C.byref(nb),
+                                                     None), "stage_f32")
+        torch.cuda.synchronize()
+        return t
+
+    def calibrate(self, x: torch.Tensor, qmax: float = 127.0) -> None:
+        """Set every activation scale from the GPU fp32 reference forward over
+        x (dlq_resnet18_calibrate) and prepare again."""
+        from .lib import stream_handle
+        self._check(self._lib.dlq_resnet18_calibrate(self.h, x.data_ptr(), x.shape[0], float(qmax), stream_handle()),
+                    "resnet18_calibrate")
+        self._check(self._lib.dlq_resnet18_prepare(self.h, self.max_batch, None), "resnet18_prepare")
+
+    def scales(self, path: str) -> None:
+        """Write the current activation scales (dlq_resnet18_load_scales format)."""
+        self._check(self._lib.dlq_resnet18_save_scales(self.h, path.encode()), "save_scales")
 
     def set_timing(self, on: bool):
         self._check(self._lib.dlq_resnet18_set_timing(self.h, int(on)), "set_timing")
@@ -271,3 +304,39 @@ def mlp_weights(inp=784, hidden=256, out=10, seed=12345):
     b1 = (rng.random(hidden, dtype=np.float32) * 0.02 - 0.01).astype(np.float32)
     b2 = (rng.random(out, dtype=np.float32) * 0.02 - 0.01).astype(np.float32)
     return W1, b1, W2, b2
+
+
+# ------------------------------------------------------- MNIST fp32 CPU path
+
+class MNISTMLP(nn.Module):
+    """BASELINE configs[0]: the reference's 2-layer MLP in PyTorch on the CPU
+    (CUDA/MNIST_on_GPU/v1.py:35-47: fc1 -> ReLU -> fc2, 784 -> hidden -> 10),
+    built from [in][out] weights as the reference's C/CUDA versions store
+    them (v4.cu:95-107; nn.Linear keeps [out][in], hence the transposes).
+    The plumbing baseline beside the int8 MLP on the GPU (MLPInt8); not part
+    of the int8 engine."""
+
+    def __init__(self, W1, b1, W2, b2):
+        super().__init__()
+        inp, hidden = W1.shape
+        out = W2.shape[1]
+        self.fc1 = nn.Linear(inp, hidden)
+        self.relu = nn.ReLU()
+        self.fc2 = nn.Linear(hidden, out)
+        with torch.no_grad():
+            self.fc1.weight.copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(W1, np.float32).T)))
+            self.fc1.bias.copy_(torch.from_numpy(np.asarray(b1, np.float32)))
+            self.fc2.weight.copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(W2, np.float32).T)))
+            self.fc2.bias.copy_(torch.from_numpy(np.asarray(b2, np.float32)))
+
+    def forward(self, x):
+        x = x.reshape(x.shape[0], -1)  # v1.py:43 (x.reshape(batch_size, 28 * 28))
+        return self.fc2(self.relu(self.fc1(x)))
+
+
+def mnist_inputs(B: int, seed: int = 7) -> np.ndarray:
+    """Synthetic MNIST-shaped batch [B,784]: seeded u8 pixels /255, normalised
+    with the reference's mean/std (v1.py:21-24); the data files are absent."""
+    rng = np.random.default_rng(seed)
+    x = rng.integers(0, 256, size=(B, 784), dtype=np.uint8).astype(np.float32) / np.float32(255.0)
+    return ((x - np.float32(0.1307)) / np.float32(0.3081)).astype(np.float32)

@@ -297,16 +297,16 @@ int dlq_resnet18_load_scales(dlq_resnet18* m, const char* path);
 int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream);
 /* logits[B][1000] fp32 (device) from x[B][3][224][224] fp32 NCHW (device). */
 int dlq_resnet18_forward(dlq_resnet18* m, const float* x, int B, float* logits, void* stream);
-/* Keep snapshots of every stage output (for dumps/parity; costs D2D copies
- * inside forward).  Takes effect at the next dlq_resnet18_prepare. */
 /* basic_block_forward (RK/runtime/infer_e2e.cu:139-203) of block 0..7
  * (layer1.0 .. layer4.1) of a prepared model on int8 NHWC x (scale of the
  * block input) -> int8 NHWC y (scale of the block's conv2); intermediates
  * live in the model's workspace (do not overlap with a forward). */
 int dlq_basic_block_s8(dlq_resnet18* m, int block, const int8_t* x, int N, int8_t* y, void* stream);
+/* Keep snapshots of every stage output (for dumps/parity; costs D2D copies
+ * inside forward).  Takes effect at the next dlq_resnet18_prepare. */
 int dlq_resnet18_set_keep_stages(dlq_resnet18* m, int on);
 /* Copy a stage activation of the last forward to device memory `dst`:
- * "input_q", "conv1", "stem_pool", "layer1".."layer4" (int8 NHWC) or
+ * "stem_pool", "layer1".."layer4" (int8 NHWC) or
  * "gap" (int8 [B][512]).  *bytes receives the size. */
 int dlq_resnet18_stage(dlq_resnet18* m, const char* name, void* dst, size_t cap, size_t* bytes,
                        void* stream);
@@ -322,10 +322,10 @@ int dlq_resnet18_stage(dlq_resnet18* m, const char* name, void* dst, size_t cap,
 enum {
   DLQ_FAM_STEM = 0,  /* stem_fused_kernel: quantise + conv1 + BN/ReLU + maxpool */
   DLQ_FAM_L1 = 1,    /* block_l1_kernel: fused layer1 basic blocks             */
-  DLQ_FAM_S2DS = 2,  /* conv3x3s2_kernel: layerX.0 conv1 + fused downsample     */
-  DLQ_FAM_WIDE = 3,  /* conv3x3w_kernel: layer2-4 stride-1 3x3 convs            */
-  DLQ_FAM_GAP = 4,   /* gap16_kernel                                            */
-  DLQ_FAM_FC = 5,    /* linear_kernel (FC)                                      */
+  DLQ_FAM_S2DS = 2,  /* conv3x3s2i_kernel: layerX.0 conv1 + fused downsample    */
+  DLQ_FAM_WIDE = 3,  /* conv3x3i_kernel: layer2-4 stride-1 3x3 convs            */
+  DLQ_FAM_GAP = 4,   /* gap_fc_kernel (int8: GAP + FC) / gap16 (fp8, split)     */
+  DLQ_FAM_FC = 5,    /* linear_kernel (FC, when the head is split)              */
   DLQ_FAM_OTHER = 6, /* any unfused fallback launch                             */
   DLQ_FAM_F8 = 7,    /* conv_s8_kernel<..., F8>: every conv of the fp8 path     */
   DLQ_FAM_COUNT = 8
@@ -335,6 +335,23 @@ int dlq_resnet18_timing(dlq_resnet18* m, double* ms, int* launches, int* forward
 int dlq_resnet18_family_work(const dlq_resnet18* m, double* macs, double* bytes);
 /* Algorithmic MACs per image of the 20 convs and of the FC layer. */
 int dlq_resnet18_macs_per_image(const dlq_resnet18* m, double* conv_macs, double* fc_macs);
+
+/* The reference's fp32 forward, op for op (RK/runtime/infer_e2e.cu:259-438:
+ * im2col-ordered fmaf GEMM convs, bn_inference, relu, add_inplace, maxpool,
+ * gap_global_ref, fc_forward + host bias), on the GPU from the model's fp32
+ * tensors (an int8 manifest's weights as q * scale): logits[B][1000] fp32
+ * (device, nullable) from x[B][3][224][224] (device).  Bit-identical to the
+ * reference's fp32 semantics (pinned by out/step8_logits.bin via the oracle);
+ * naive kernels -- model preparation and parity, not the int8 hot path.
+ * Keeps "stem_pool", "layer1".."layer4", "gap", "logits" (fp32 NCHW) for
+ * dlq_resnet18_stage_f32.  Synchronous. */
+int dlq_resnet18_forward_f32(dlq_resnet18* m, const float* x, int B, float* logits, void* stream);
+int dlq_resnet18_stage_f32(dlq_resnet18* m, const char* name, void* dst, size_t cap, size_t* bytes, void* stream);
+/* Activation-scale calibration (the "quant block" of RK reports/Step1.md:92):
+ * dlq_resnet18_forward_f32 over x[B] and every site's scale set to
+ * float(max(amax, 1e-8) / qmax) (qmax 127 for int8, 448 for fp8).  Needs a
+ * new dlq_resnet18_prepare afterwards.  Synchronous. */
+int dlq_resnet18_calibrate(dlq_resnet18* m, const float* x, int B, float qmax, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* MNIST MLP (CUDA/MNIST_on_GPU/v4.cu forward_timed :255-302, v5.cu        */

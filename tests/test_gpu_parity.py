@@ -216,19 +216,21 @@ def test_maxpool_and_gap_bitexact(gpu):
     assert np.array_equal(ggot, gref)
 
 
-@pytest.mark.parametrize("N,HW,OC", [(1, 49, 1000), (5, 49, 1000), (256, 49, 1000), (7, 1, 1000), (6, 56, 64),
-                                     (3, 17, 10)])
-def test_gap_fc_fused_head_bitexact(gpu, N, HW, OC):
+@pytest.mark.parametrize("N,HW,OC,lo", [(1, 49, 1000, 0), (5, 49, 1000, 0), (256, 49, 1000, 0), (7, 1, 1000, 0),
+                                        (6, 56, 64, 0), (3, 17, 10, 0), (5, 49, 1000, -128), (4, 1, 1000, -128)])
+def test_gap_fc_fused_head_bitexact(gpu, N, HW, OC, lo):
     """gap_fc_kernel (one launch) == oracle GAP then FC, bit for bit, on ragged
-    image groups (N % 4 != 0), HW from 1 to its 56 maximum and OC tails."""
+    image groups (N % 4 != 0), HW from 1 to its 56 maximum and OC tails; lo =
+    -128: signed bytes (every code, -128 included) and GAP codes saturating at
+    -127 (HW = 1, where the mean is the byte itself)."""
     from dlq_amd import ops
     from tests.helpers import golden
     rng = np.random.default_rng(N * 131 + HW)
     W = golden("fc.weight.bin", (1000, 512))[:OC]  # the reference's real FC weights (tmp_e2e/)
     bias = golden("fc.bias.bin")[:OC]
     wq, sw = O.quantize_weights_s8(W)
-    x = rand_s8(rng, (N, 512, 1, HW), lo=0)  # post-ReLU int8 layer4 output, NCHW
-    k = O.gap_k(0.05, HW, 0.011)
+    x = rand_s8(rng, (N, 512, 1, HW), lo=lo)  # int8 layer4 output (post-ReLU for lo = 0), NCHW
+    k = O.gap_k(0.05, HW, 0.011 if lo == 0 else 0.04)
     g, _ = O.gap_s8(x, k)
     alpha = O.fc_alpha(0.011, sw)
     ref, _ = O.fc_s8(g, wq, alpha, bias)

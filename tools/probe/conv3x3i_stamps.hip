@@ -2,6 +2,7 @@
 // wide stride-1 conv kernel (conv3x3i.hip), random int8 data.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DDLQ_STAMPS \
 //          -I dlq_amd/csrc tools/probe/conv3x3i_stamps.hip -o tools/probe/conv3x3i_stamps
+#define DLQ_ABLATION 1  // the kernel honours a.dbg (timing ablations)
 #include <cstdio>
 #include <cstdlib>
 #include <vector>

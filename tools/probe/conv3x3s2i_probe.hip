@@ -3,6 +3,7 @@
 // int8 data, B = 256; argv: OW (28/14/7), dbg bits (2 = no LDS-DMA).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //          -I dlq_amd/csrc tools/probe/conv3x3s2i_probe.hip -o tools/probe/conv3x3s2i_probe
+#define DLQ_ABLATION 1  // the kernel honours a.dbg (timing ablations)
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
