@@ -119,6 +119,25 @@ __device__ __forceinline__ void wave_tiles(int wave, int& mt, int& f0, int& nf) 
 // slice at twice the i8 MFMA's cycles, 10/9 of the int8 MFMA time), B
 // fragments stream through a 3-deep register ring (the doubled fragment
 // would not fit next to the fp32 accumulators otherwise).
+// The kernel's LDS constants (zero region, alpha/beta): written after stage
+// 0's DMA is issued so their global-load latency overlaps it; stage 0's
+// barrier publishes them.
+template <int W, int C, int OUT>
+__device__ __forceinline__ void conv3x3i_init(const ConvArgs& a, int8_t* lds) {
+  using G = IGeo<W>;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < G::ZU * 4; i += INW * 64) {
+    ((int*)(lds + G::OFF_Z))[i] = 0;
+    ((int*)(lds + G::SLOT + G::OFF_Z))[i] = 0;
+  }
+  if constexpr (OUT == 0) {
+    for (int i = tid; i < a.OCp; i += INW * 64) {
+      ((float*)(lds + G::OFF_AB))[i] = a.alpha[i];
+      ((float*)(lds + G::OFF_AB))[C + i] = a.beta[i];
+    }
+  }
+}
+
 template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false>
 __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int mt, int f0, int lrank) {
   using G = IGeo<W>;
@@ -236,6 +255,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #pragma unroll
     for (int k = 0; k < DPW; ++k) issue_piece(0, k);
   }
+  conv3x3i_init<W, C, OUT>(a, lds);
 
   for (int s = 0; s < nst; ++s) {
     const int li = s / NS, j = s - li * NS;
@@ -452,17 +472,6 @@ __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
   const int tid = threadIdx.x;
-  if constexpr (OUT == 0) {
-    for (int i = tid; i < a.OCp; i += INW * 64) {
-      ((float*)(lds + OFF_AB))[i] = a.alpha[i];
-      ((float*)(lds + OFF_AB))[C + i] = a.beta[i];
-    }
-  }
-  for (int i = tid; i < G::ZU * 4; i += INW * 64) {
-    ((int*)(lds + G::OFF_Z))[i] = 0;
-    ((int*)(lds + G::SLOT + G::OFF_Z))[i] = 0;
-  }
-  __syncthreads();
   int mt, f0, nf;
   const int wave = tid >> 6;
   wave_tiles<G::MT>(wave, mt, f0, nf);

@@ -135,8 +135,8 @@ __device__ __forceinline__ int perm_at(int slot) {
 }
 
 template <int OW, int C, int OUT, bool DS, int NF, bool F8, bool RW>
-__device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, int8_t* y_ds, int8_t* lds,
-                                         int mt, int f0) {
+__device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, const float* be_ds,
+                                         int8_t* y_ds, int8_t* lds, int mt, int f0) {
   using G = JGeo<OW, DS, RW ? C / JSC : 0>;
   constexpr int NS = C / JSC, OC = 2 * C;
   constexpr int DPW = (G::NPIECE + JNW - 1) / JNW;
@@ -239,6 +239,24 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
   Acc acc[NF], accd[DS ? NF : 1];
   int cur_ot = 0, cur_p0 = 0;
 
+  auto init = [&]() {  // LDS constants after the first DMA issue: their load latency overlaps it
+    const int t = threadIdx.x;
+    if constexpr (OUT == 0) {
+      float* ab = (float*)(lds + G::OFF_AB);
+      for (int i = t; i < a.OCp; i += JNW * 64) {
+        ab[i] = a.alpha[i];
+        ab[OC + i] = a.beta[i];
+        if constexpr (DS) {
+          ab[2 * OC + i] = al_ds[i];
+          ab[3 * OC + i] = be_ds[i];
+        }
+      }
+    }
+    for (int i = t; i < G::ZU * 4; i += JNW * 64) {
+      ((int*)(lds + G::OFF_Z))[i] = 0;
+      ((int*)(lds + G::SLOT + G::OFF_Z))[i] = 0;
+    }
+  };
   if constexpr (RW) {  // every stage's weight block (one output-channel tile), once
     constexpr int NW = NS * G::WP;
     for (int pc = wave; pc < NW; pc += JNW) {
@@ -251,6 +269,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
   prep_for(0);
 #pragma unroll
   for (int k = 0; k < DPW; ++k) issue_piece(0, k);
+  init();  // published by stage 0's barrier
 
   for (int s = 0; s < nst; ++s) {
     const int li = s / NS, j = s - li * NS;
@@ -449,28 +468,11 @@ __global__ __launch_bounds__(JNW * 64, 1) void conv3x3s2i_kernel(ConvArgs a, con
   constexpr int LDS_TOTAL = G::OFF_AB + (DS ? 4 : 2) * OC * 4;
   static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
-  const int tid = threadIdx.x;
-  if constexpr (OUT == 0) {
-    float* ab = (float*)(lds + G::OFF_AB);
-    for (int i = tid; i < a.OCp; i += JNW * 64) {
-      ab[i] = a.alpha[i];
-      ab[OC + i] = a.beta[i];
-      if constexpr (DS) {
-        ab[2 * OC + i] = al_ds[i];
-        ab[3 * OC + i] = be_ds[i];
-      }
-    }
-  }
-  for (int i = tid; i < G::ZU * 4; i += JNW * 64) {
-    ((int*)(lds + G::OFF_Z))[i] = 0;
-    ((int*)(lds + G::SLOT + G::OFF_Z))[i] = 0;
-  }
-  __syncthreads();
-  const int wave = tid >> 6;
+  const int wave = threadIdx.x >> 6;
   if (wave < 4)
-    s2i_body<OW, C, OUT, DS, 4, F8, RW>(a, w_ds, y_ds, lds, wave & 3, 0);
+    s2i_body<OW, C, OUT, DS, 4, F8, RW>(a, w_ds, al_ds, be_ds, y_ds, lds, wave & 3, 0);
   else
-    s2i_body<OW, C, OUT, DS, 3, F8, RW>(a, w_ds, y_ds, lds, wave & 3, 4);
+    s2i_body<OW, C, OUT, DS, 3, F8, RW>(a, w_ds, al_ds, be_ds, y_ds, lds, wave & 3, 4);
 }
 
 int num_cus_s2i() {

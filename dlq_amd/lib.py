@@ -15,7 +15,9 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdlq.so")
+# DLQ_LIB_PATH: load another build of the same library (A/B timing of two
+# builds on one box); the default is the in-tree dlq_amd/libdlq.so.
+LIB_PATH = os.environ.get("DLQ_LIB_PATH") or os.path.join(_HERE, "libdlq.so")
 
 DLQ_OK = 0
 DLQ_OUT_S8, DLQ_OUT_F32, DLQ_OUT_S32 = 0, 1, 2
