@@ -7,8 +7,8 @@
 //
 // Tile 256 x 256 per 512-thread workgroup (8 waves = 2 (M) x 4 (N), each 128 x
 // 64 = 4 x 2 v_mfma_i32_32x32x32_i8 tiles), K = 64 per stage, double-buffered
-// LDS (2 x 40 KiB), one barrier per stage: the next stage's global loads are
-// in flight in registers while this stage's MFMAs run.
+// LDS (2 x 40 KiB), one barrier per stage; global loads run two stages ahead
+// in two register sets, so each has two stages of MFMAs to land.
 //  * A rows are K-contiguous, as the MFMA wants: 16-byte loads straight into
 //    LDS rows [m][64 k].
 //  * B is N-contiguous in memory but the MFMA's B operand is K-contiguous per
@@ -39,7 +39,7 @@ __device__ __forceinline__ unsigned ld_bytes(const int8_t* p, int avail) {  // u
   return v;
 }
 
-__global__ __launch_bounds__(512, 1) void gemm_s8s8s32_kernel(const int8_t* __restrict__ A,
+__global__ __launch_bounds__(512, 1) void gemm_s8s8s32_generic_kernel(const int8_t* __restrict__ A,
                                                              const int8_t* __restrict__ B, int32_t* __restrict__ C,
                                                              int M, int N, int K, int nbn, int aligned) {
   __shared__ __attribute__((aligned(16))) int8_t lds[2 * GSLOT];
@@ -52,18 +52,22 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_kernel(const int8_t* __re
   // A: rows (tid >> 2) and +128, 16-byte chunk tid & 3; B: 8 columns 8 * (tid & 31), rows 4 * (tid >> 5) .. +3
   const int a_row = tid >> 2, a_ch = tid & 3;
   const int b_cg = tid & 31, b_rq = tid >> 5;
-  v4i ra[2];
-  unsigned rb[4][2];
+  // Two stages of global loads in flight in registers: set (s & 1) holds
+  // stage s + 1 while stage s + 2's loads are issued into the other set, so
+  // each load has two stages of MFMAs to land before its LDS write.
+  v4i ra[2][2];
+  unsigned rb[2][4][2];
 
-  auto gload = [&](int k0) {
+  auto gload = [&](int k0, int set) {
     if (full_mn && k0 + GK <= K) {
 #pragma unroll
-      for (int p = 0; p < 2; ++p) ra[p] = *(const v4i*)(A + (size_t)(m0 + a_row + 128 * p) * K + k0 + a_ch * 16);
+      for (int p = 0; p < 2; ++p)
+        ra[set][p] = *(const v4i*)(A + (size_t)(m0 + a_row + 128 * p) * K + k0 + a_ch * 16);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const uint2 v = *(const uint2*)(B + (size_t)(k0 + 4 * b_rq + r) * N + n0 + 8 * b_cg);
-        rb[r][0] = v.x;
-        rb[r][1] = v.y;
+        rb[set][r][0] = v.x;
+        rb[set][r][1] = v.y;
       }
       return;
     }
@@ -72,44 +76,35 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_kernel(const int8_t* __re
       const int m = m0 + a_row + 128 * p, k = k0 + a_ch * 16;
       const int8_t* src = A + (size_t)m * K + k;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) ra[p][w] = (int)(m < M ? ld_bytes(src + 4 * w, K - k - 4 * w) : 0u);
+      for (int w = 0; w < 4; ++w) ra[set][p][w] = (int)(m < M ? ld_bytes(src + 4 * w, K - k - 4 * w) : 0u);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int k = k0 + 4 * b_rq + r, n = n0 + 8 * b_cg;
       const int8_t* src = B + (size_t)k * N + n;
-      rb[r][0] = k < K ? ld_bytes(src, N - n) : 0u;
-      rb[r][1] = k < K ? ld_bytes(src + 4, N - n - 4) : 0u;
+      rb[set][r][0] = k < K ? ld_bytes(src, N - n) : 0u;
+      rb[set][r][1] = k < K ? ld_bytes(src + 4, N - n - 4) : 0u;
     }
   };
-  auto lstore = [&](int slot) {
+  auto lstore = [&](int slot, int set) {
     int8_t* la = lds + slot * GSLOT;
     int8_t* lb = la + GT * GP;
 #pragma unroll
-    for (int p = 0; p < 2; ++p) *(v4i*)(la + (a_row + 128 * p) * GP + a_ch * 16) = ra[p];
+    for (int p = 0; p < 2; ++p) *(v4i*)(la + (a_row + 128 * p) * GP + a_ch * 16) = ra[set][p];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {  // 4 x 4 byte transpose: rows k..k+3 -> column dwords
-      const unsigned t0 = __builtin_amdgcn_perm(rb[1][h], rb[0][h], 0x05010400u);
-      const unsigned t1 = __builtin_amdgcn_perm(rb[1][h], rb[0][h], 0x07030602u);
-      const unsigned t2 = __builtin_amdgcn_perm(rb[3][h], rb[2][h], 0x05010400u);
-      const unsigned t3 = __builtin_amdgcn_perm(rb[3][h], rb[2][h], 0x07030602u);
+      const unsigned t0 = __builtin_amdgcn_perm(rb[set][1][h], rb[set][0][h], 0x05010400u);
+      const unsigned t1 = __builtin_amdgcn_perm(rb[set][1][h], rb[set][0][h], 0x07030602u);
+      const unsigned t2 = __builtin_amdgcn_perm(rb[set][3][h], rb[set][2][h], 0x05010400u);
+      const unsigned t3 = __builtin_amdgcn_perm(rb[set][3][h], rb[set][2][h], 0x07030602u);
       const unsigned d[4] = {__builtin_amdgcn_perm(t2, t0, 0x05040100u), __builtin_amdgcn_perm(t2, t0, 0x07060302u),
                              __builtin_amdgcn_perm(t3, t1, 0x05040100u), __builtin_amdgcn_perm(t3, t1, 0x07060302u)};
 #pragma unroll
       for (int c = 0; c < 4; ++c) *(unsigned*)(lb + (8 * b_cg + 4 * h + c) * GP + 4 * b_rq) = d[c];
     }
   };
-
-  v16i acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = v16i{0};
-  const int nst = (K + GK - 1) / GK;
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int s = 0; s < nst; ++s) {
-    if (s + 1 < nst) gload((s + 1) * GK);
-    const int8_t* la = lds + (s & 1) * GSLOT;
+  auto compute = [&](int slot, v16i (&acc)[4][2]) {
+    const int8_t* la = lds + slot * GSLOT;
     const int8_t* lb = la + GT * GP;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -123,10 +118,138 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_kernel(const int8_t* __re
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    if (s + 1 < nst) lstore((s + 1) & 1);
+  };
+
+  v16i acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = v16i{0};
+  const int nst = (K + GK - 1) / GK;
+  gload(0, 0);
+  if (nst > 1) gload(GK, 1);
+  lstore(0, 0);
+  __syncthreads();
+  // iteration s: stage s + 2's loads into register set s & 1 (its stage s
+  // went to LDS one iteration ago), stage s from LDS slot s & 1, then stage
+  // s + 1 (set (s + 1) & 1, landed during this stage) into the other slot.
+  int s = 0;
+  for (; s + 1 < nst; s += 2) {  // unrolled by two so the register sets are compile-time
+    if (s + 2 < nst) gload((s + 2) * GK, 0);
+    compute(0, acc);
+    lstore(1, 1);
+    __syncthreads();
+    if (s + 3 < nst) gload((s + 3) * GK, 1);
+    compute(1, acc);
+    if (s + 2 < nst) lstore(0, 0);
     __syncthreads();
   }
+  if (s < nst) compute(0, acc);  // odd stage count: the last stage sits in slot 0
   // D reg r, lane (lr, lh): row (r & 3) + 8 (r >> 2) + 4 lh, column lr of the 32 x 32 tile
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + lr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M && n < N) C[(size_t)m * N + n] = acc[i][j][r];
+      }
+    }
+}
+
+
+// ---- aligned operands (K % 16 == 0, N % 16 == 0, 16-byte aligned bases):
+// both tiles stream by LDS-DMA through a 4-slot ring, three stages ahead.
+//  * A image: row m, 16-byte chunk c of its 64 K bytes at m*64 + 16*(c ^
+//    ((m >> 2) & 3)) -- a ds_read_b128 lane group's 16 rows hit 16 bank quads.
+//  * B image: K rows of 256 N bytes as loaded (no register transpose): chunk b
+//    of row k at k*256 + 16*(b ^ 2(k & 7)).  The MFMA B fragment (16 K bytes
+//    of one column) is two ds_read_b64_tr_b8: per 16-lane group, lane 2q + p
+//    addresses row q (of 8), columns 8p .. 8p+7, and lane i receives column
+//    i's 8 row bytes (probed on gfx950); the XOR puts a 32-lane half's 8 rows
+//    x 32 columns on 64 distinct banks.
+//  * The swizzles are applied on the global side: DMA lane t of a piece
+//    fetches the global chunk whose swizzled LDS position is t.
+constexpr int GSLOTS = 4;
+constexpr int GSLOT_A = GT * GK;           // 16 KiB
+constexpr int GSLOT_B = GK * GT;           // 16 KiB
+constexpr int GSLOT_DMA = GSLOT_A + GSLOT_B;
+
+__device__ __attribute__((aligned(64))) int8_t g_zero_gemm[64];
+
+typedef int v2i __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2i ds_tr8(const int8_t* p) {
+  return __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)p);
+}
+
+__global__ __launch_bounds__(512, 1) void gemm_s8s8s32_kernel(const int8_t* __restrict__ A,
+                                                             const int8_t* __restrict__ B, int32_t* __restrict__ C,
+                                                             int M, int N, int K, int nbn) {
+  __shared__ __attribute__((aligned(16))) int8_t lds[GSLOTS * GSLOT_DMA];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int l = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (l / nbn) * GT, n0 = (l % nbn) * GT;
+  const int wm = wave >> 2, wn = wave & 3;
+  const unsigned lds32 = lds_addr32(lds);
+  const int nst = (K + GK - 1) / GK;
+
+  // DMA pieces of a stage: 16 for A (piece j = rows 16j .. 16j+15), 16 for B
+  // (piece j = rows 4j .. 4j+3); wave w issues pieces w, w+8, w+16, w+24.
+  auto issue = [&](int st) {
+    const int k0 = st * GK;
+    const unsigned slot = lds32 + (st % GSLOTS) * GSLOT_DMA;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int pc = wave + 8 * r;
+      const int t = (pc & 15) * 64 + lane;  // chunk index in the image
+      const int8_t* src;
+      if (pc < 16) {
+        const int m = t >> 2, c = (t & 3) ^ ((m >> 2) & 3), k = k0 + 16 * c;
+        src = (m0 + m < M && k < K) ? A + (size_t)(m0 + m) * K + k : g_zero_gemm;
+        glds16_asm(src, slot + (pc & 15) * 1024);
+      } else {
+        const int k = t >> 4, b = (t & 15) ^ (2 * (k & 7)), n = n0 + 16 * b;
+        src = (k0 + k < K && n < N) ? B + (size_t)(k0 + k) * N + n : g_zero_gemm;
+        glds16_asm(src, slot + GSLOT_A + (pc & 15) * 1024);
+      }
+    }
+  };
+
+  v16i acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = v16i{0};
+  for (int st = 0; st < 3 && st < nst; ++st) issue(st);
+  const int q = (lane & 15) >> 1, p = lane & 1, g = (lane >> 4) & 1;
+  for (int s = 0; s < nst; ++s) {
+    const int younger = nst - 1 - s < 2 ? nst - 1 - s : 2;  // stages issued after s (4 pieces each)
+    wait_vm(4 * younger);
+    __builtin_amdgcn_s_barrier();
+    if (s + 3 < nst) issue(s + 3);  // into the slot stage s - 1 left
+    const int8_t* la = lds + (s % GSLOTS) * GSLOT_DMA;
+    const int8_t* lb = la + GSLOT_A;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      v4i fa[4], fb[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = wm * 128 + i * 32 + lr, c = ks * 2 + lh;
+        fa[i] = *(const v4i*)(la + m * 64 + 16 * (c ^ ((m >> 2) & 3)));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int k = ks * 32 + lh * 16 + q, b = wn * 4 + j * 2 + g;
+        const int8_t* a0 = lb + k * 256 + 16 * (b ^ (2 * (k & 7))) + 8 * p;
+        const v2i lo = ds_tr8(a0), hi = ds_tr8(a0 + 8 * 256);
+        fb[j] = v4i{lo[0], lo[1], hi[0], hi[1]};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -146,8 +269,13 @@ hipError_t launch_gemm_s8s8s32(const int8_t* A, const int8_t* B, int32_t* C, int
   const int nbm = (M + GT - 1) / GT, nbn = (N + GT - 1) / GT;
   const long tiles = (long)nbm * nbn;
   if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
-  const int aligned = K % 16 == 0 && N % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 7) == 0;
-  hipLaunchKernelGGL(gemm_s8s8s32_kernel, dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M, N, K, nbn, aligned);
+  if (K % 16 == 0 && N % 16 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0) {
+    hipLaunchKernelGGL(gemm_s8s8s32_kernel, dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M, N, K, nbn);
+  } else {
+    const int aligned = K % 16 == 0 && N % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 7) == 0;
+    hipLaunchKernelGGL(gemm_s8s8s32_generic_kernel, dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M, N, K, nbn,
+                       aligned);
+  }
   return hipGetLastError();
 }
 

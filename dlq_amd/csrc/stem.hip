@@ -7,8 +7,11 @@
 // and maxpool2d_3x3_s2p1_nchw (:282-293).  The 112x112x64 conv1 output never
 // leaves the register file.
 //
-// Input: the fp32 rows stream through an LDS-DMA ring and are quantised into a
-// ring of "super rows": 2x2 pixels x (RGB, 0) = 16-byte super-pixels, so the
+// Input: every thread loads the fp32 values of its half super-pixel straight
+// into registers (three 8-byte loads, one per channel: 64 lanes read 512
+// contiguous bytes of an input row), PD steps ahead of their use, and
+// quantises them into a ring of "super rows": 2x2 pixels x (RGB, 0) = 16-byte
+// super-pixels, so the
 // 7x7/s2 conv is a 4x4/s1 conv over super-pixels (kh = 2*ky+dy-1; kh = -1
 // carries a zero weight) with K = 16 super taps x 16 B = 8 steps of
 // v_mfma_i32_32x32x32_i8, every A fragment one ds_read_b128.
@@ -30,6 +33,7 @@
 // computes conv rows 2p, 2p+1 and emits pooled row p.
 #include <cmath>
 #include <type_traits>
+#include <utility>
 
 #include "device_common.h"
 
@@ -37,15 +41,14 @@ namespace dlq {
 namespace {
 
 constexpr int SNW = 8;                   // waves
-constexpr int SLA = 6;                   // raw-row pairs in flight ahead of the converter (>= 3)
-constexpr int RAW_SLOTS = SLA + 1;       // raw ring: pairs of super rows (12 x 1 KiB input rows)
-constexpr int RAW_SLOT_BYTES = 12 * 1024;
+constexpr int PD = 2;                    // super-row pairs whose input loads are in flight ahead of the converter
 constexpr int PATCH_SLOTS = 8;           // super-row ring
 constexpr int PATCH_ROW = 128 * 16;      // super cols -4 .. 123
-constexpr int OFF_RAW = 0;
-constexpr int OFF_PATCH = OFF_RAW + RAW_SLOTS * RAW_SLOT_BYTES;
+constexpr int OFF_PATCH = 0;
 constexpr int OFF_STAGE = OFF_PATCH + PATCH_SLOTS * PATCH_ROW;  // per wave 16 x 32 B output staging
-constexpr int LDS_STEM = OFF_STAGE + SNW * 512;
+constexpr int WPITCH_S = 256 + 16;       // weight row pitch (17 units: a lane group's 16 rows on 16 bank quads)
+constexpr int OFF_WST = OFF_STAGE + SNW * 512;                  // the 64 x 256 B weight image
+constexpr int LDS_STEM = OFF_WST + 64 * WPITCH_S;               // 37 KiB: two workgroups per CU
 static_assert(LDS_STEM <= 160 * 1024, "LDS budget");
 constexpr int kIntMin = (int)0x80000000;
 
@@ -96,7 +99,7 @@ __device__ __forceinline__ int max3i(int a, int b, int c) {
 // alpha >= 0: dlq_pack_stem_weights_f8 flips the sign bits of the rows with
 // alpha < 0).
 template <bool F8>
-__global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
+__global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
   using Acc = typename std::conditional<F8, v16f, v16i>::type;
   using Pv = typename std::conditional<F8, float, int>::type;
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_STEM];
@@ -104,18 +107,15 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 31, lh = lane >> 5;
   const int ot = wave & 1, q = wave >> 1;  // channel tile, column quarter
-  const int D = wave < 4 ? 2 : 1;          // raw DMA pieces per pair issued by this wave
   const int nitems = a.N * a.nb;
 
-  // B fragments (weights) for all 8 k-steps, and the channel's epilogue constants.
-  v4i wreg[8];
-  {
-    const int8_t* wp = a.w + (ot * 32 + lr) * 256 + lh * 16;
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) wreg[kk] = *(const v4i*)(wp + kk * 32);
-  }
+  // The weight image in LDS (B fragments re-read per conv row: registers go to
+  // the second co-resident workgroup), and the channel's epilogue constants.
+  for (int i = tid; i < 64 * 16; i += SNW * 64)
+    *(v4i*)(lds + OFF_WST + (i >> 4) * WPITCH_S + (i & 15) * 16) = *(const v4i*)(a.w + i * 16);
+  const int8_t* wlds = lds + OFF_WST + (ot * 32 + lr) * WPITCH_S + lh * 16;
   const float al = a.alpha[ot * 32 + lr], be = a.beta[ot * 32 + lr];
-  wait_vm_const<0>();  // before any LDS-DMA is counted
+  __syncthreads();
   // A-row permutation: lane row i -> conv column offset pi(i) (D reg r of half h = column 16h + r)
   const int pi = ((lr >> 3) << 2) + (lr & 3) + 16 * ((lr >> 2) & 1);
   const int a_unit = 28 * q + 1 + pi;  // super-col unit of tap kx = 0 (unit = super col + 4)
@@ -129,80 +129,112 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
     const int sr0 = 2 * py0 - 3;  // first super row (pair k = super rows sr0+2k, sr0+2k+1)
     const float* img = a.x + (size_t)n * 3 * 224 * 224;
 
-    // Raw pair k -> ring slot k % RAW_SLOTS: 12 input rows (2 super rows x 3
-    // channels x 2 pixel rows), 896 B each in a 1 KiB piece.  Waves 0-3 issue
-    // two pieces per pair, waves 4-7 one.
-    auto issue_pair = [&](int k) {
-      const unsigned slot = lds32 + OFF_RAW + (k % RAW_SLOTS) * RAW_SLOT_BYTES;
+    // Super-row pair k = super rows sr0+2k, sr0+2k+1.  Thread = (pixel row
+    // dy, super row h of the pair, unit): unit = super col + 4 (units 0..3
+    // and 116..127 are the zero border); its input = channels 0..2 x pixels
+    // (2 sc, 2 sc + 1) of image row 2 sr + dy: three float2 loads.  Pair k's
+    // loads sit in register set k % (PD + 1) (compile-time: the step loop is
+    // unrolled by PD + 1) until convert_pair quantises them into the patch.
+    const int cv_unit = tid & 127, cv_h = (tid >> 7) & 1, cv_dy = tid >> 8, cv_sc = cv_unit - 4;
+    using F2 = float __attribute__((ext_vector_type(2)));
+    F2 raw[PD + 1][3];
+    auto load_pair = [&](int k, F2 (&r)[3]) {
+      const int sr = sr0 + 2 * k + cv_h;
+      if ((unsigned)sr < 112u && (unsigned)cv_sc < 112u) {
+        const float* src = img + (size_t)(2 * sr + cv_dy) * 224 + 2 * cv_sc;
 #pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        const int j = wave + 8 * d;
-        if (j < 12) {
-          const int sr = sr0 + 2 * k + j / 6, c = (j % 6) >> 1, dy = j & 1;
-          const bool ok = (unsigned)sr < 112u;
-          const int l = lane < 56 ? lane : 55;
-          const float* src = ok ? img + ((size_t)c * 224 + 2 * sr + dy) * 224 + l * 4 : a.x;
-          glds16_asm(src, slot + j * 1024);
-        }
-      }
-    };
-    // Quantise raw pair k into two super rows of the patch ring, all 8 waves:
-    // thread = (pixel row dy, super row h, unit); 128 units = super cols
-    // -4..123; each thread writes the 8 bytes of its dy (dx = 0, 1).
-    auto convert_pair = [&](int k) {
-      const int unit = tid & 127, h = (tid >> 7) & 1, dy = tid >> 8, sc = unit - 4;
-      const int sr = sr0 + 2 * k + h;
-      int2 out = {0, 0};
-      if ((unsigned)sr < 112u && (unsigned)sc < 112u) {
-        const int8_t* raw = lds + OFF_RAW + (k % RAW_SLOTS) * RAW_SLOT_BYTES + h * 6 * 1024 + sc * 8;
-        if constexpr (F8) {  // (c0, c1, c2, +0) e4m3 per pixel
-          float v[3][2];
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const int2 f = *(const int2*)(raw + (c * 2 + dy) * 1024);
-            v[c][0] = __int_as_float(f.x) * a.inv_s;
-            v[c][1] = __int_as_float(f.y) * a.inv_s;
-          }
-          out.x = (int)enc4_f8(v[0][0], v[1][0], v[2][0], 0.f, -448.f);
-          out.y = (int)enc4_f8(v[0][1], v[1][1], v[2][1], 0.f, -448.f);
-        } else {
-        unsigned u[3][2];  // [c][dx]: clamp(x/s) + 1.5*2^23 -> rne'd int8 in the low byte
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const int2 f = *(const int2*)(raw + (c * 2 + dy) * 1024);  // dx = 0, 1 (read as ints)
-          u[c][0] = __float_as_uint(__builtin_amdgcn_fmed3f(__int_as_float(f.x) * a.inv_s, -127.f, 127.f) +
-                                    12582912.0f);
-          u[c][1] = __float_as_uint(__builtin_amdgcn_fmed3f(__int_as_float(f.y) * a.inv_s, -127.f, 127.f) +
-                                    12582912.0f);
-        }
-#pragma unroll
-        for (int dx = 0; dx < 2; ++dx) {  // bytes (c0, c1, c2, 0)
-          const unsigned t = __builtin_amdgcn_perm(u[1][dx], u[0][dx], 0x0c0c0400u);
-          (dx ? out.y : out.x) = (int)__builtin_amdgcn_perm(u[2][dx], t, 0x0c040100u);
-        }
-        }
-      }
-      *(int2*)(lds + OFF_PATCH + (sr & (PATCH_SLOTS - 1)) * PATCH_ROW + unit * 16 + dy * 8) = out;
-    };
-    // One conv row (global row oy): the wave's 32 px x 32 oc tile, 8 k-steps.
-    auto conv_row = [&](int oy) {
-      v4i af[8];
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const int sr = oy - 2 + (kk >> 1);  // ky = kk/2, kx = 2*(kk&1) + lh
-        af[kk] = *(const v4i*)(lds + OFF_PATCH + (sr & (PATCH_SLOTS - 1)) * PATCH_ROW +
-                               (a_unit + 2 * (kk & 1) + lh) * 16);
-      }
-      Acc acc = Acc{0};
-      if constexpr (F8) {
-#pragma unroll
-        for (int kp = 0; kp < 4; ++kp)
-          acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(cat8(af[2 * kp], af[2 * kp + 1]),
-                                                                cat8(wreg[2 * kp], wreg[2 * kp + 1]), acc, 0, 0, 0,
-                                                                0, 0, 0);
+        for (int c = 0; c < 3; ++c) r[c] = *(const F2*)(src + (size_t)c * 224 * 224);
       } else {
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[kk], wreg[kk], acc, 0, 0, 0);
+        for (int c = 0; c < 3; ++c) r[c] = F2{0.f, 0.f};
+      }
+    };
+    // Quantise pair k into two super rows of the patch ring: each thread
+    // writes the 8 bytes of its dy (dx = 0, 1) of one super-pixel.
+    auto convert_pair = [&](int k, const F2 (&r)[3]) {
+      const int sr = sr0 + 2 * k + cv_h;
+      int2 out = {0, 0};
+      if ((unsigned)sr < 112u && (unsigned)cv_sc < 112u) {
+        if constexpr (F8) {  // (c0, c1, c2, +0) e4m3 per pixel
+          out.x = (int)enc4_f8(r[0][0] * a.inv_s, r[1][0] * a.inv_s, r[2][0] * a.inv_s, 0.f, -448.f);
+          out.y = (int)enc4_f8(r[0][1] * a.inv_s, r[1][1] * a.inv_s, r[2][1] * a.inv_s, 0.f, -448.f);
+        } else {
+          unsigned u[3][2];  // [c][dx]: clamp(x/s) + 1.5*2^23 -> rne'd int8 in the low byte
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx)
+              u[c][dx] = __float_as_uint(__builtin_amdgcn_fmed3f(r[c][dx] * a.inv_s, -127.f, 127.f) + 12582912.0f);
+#pragma unroll
+          for (int dx = 0; dx < 2; ++dx) {  // bytes (c0, c1, c2, 0)
+            const unsigned t = __builtin_amdgcn_perm(u[1][dx], u[0][dx], 0x0c0c0400u);
+            (dx ? out.y : out.x) = (int)__builtin_amdgcn_perm(u[2][dx], t, 0x0c040100u);
+          }
+        }
+      }
+      *(int2*)(lds + OFF_PATCH + (sr & (PATCH_SLOTS - 1)) * PATCH_ROW + cv_unit * 16 + cv_dy * 8) = out;
+    };
+    // One conv row (global row oy): the wave's 32 px x 32 oc tile, 8 k-steps.
+    // int8: fragments stream two k-steps ahead through a 3-deep ring of
+    // untracked ds_read_b128 (inline asm: the compiler can neither hoist all
+    // 16 reads nor keep them all live -- two workgroups share the registers).
+    const unsigned a_col = lds32 + OFF_PATCH + (a_unit + lh) * 16;
+    const unsigned w_row = lds32 + (unsigned)(wlds - lds);
+    auto conv_row = [&](int oy) {
+      Acc acc = Acc{0};
+      unsigned ra[4];  // super rows oy-2 .. oy+1 (ky = 0..3)
+#pragma unroll
+      for (int ky = 0; ky < 4; ++ky) ra[ky] = a_col + ((oy - 2 + ky) & (PATCH_SLOTS - 1)) * PATCH_ROW;
+      if constexpr (F8) {  // k-steps 2kp, 2kp+1 = the two halves of one 64-deep fp8 MFMA
+        v4i fa[2][2], fw[2][2];
+#define STEM_RD8(kp)                                                                                              \
+  asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(fa[(kp) & 1][0]) : "v"(ra[kp]) : "memory");                   \
+  asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(fa[(kp) & 1][1]) : "v"(ra[kp]) : "memory");                  \
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fw[(kp) & 1][0]) : "v"(w_row), "n"(64 * (kp)) : "memory");  \
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fw[(kp) & 1][1]) : "v"(w_row), "n"(64 * (kp) + 32) : "memory")
+#define STEM_K8(kp)                                                                                               \
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(fa[(kp) & 1][0]), "+v"(fa[(kp) & 1][1]), "+v"(fw[(kp) & 1][0]),        \
+               "+v"(fw[(kp) & 1][1]) : "n"((kp) + 1 < 4 ? 4 : 0) : "memory");                                     \
+  acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(cat8(fa[(kp) & 1][0], fa[(kp) & 1][1]),                       \
+                                                        cat8(fw[(kp) & 1][0], fw[(kp) & 1][1]), acc, 0, 0, 0, 0, 0, 0)
+        STEM_RD8(0);
+        STEM_RD8(1);
+        STEM_K8(0);
+        STEM_RD8(2);
+        STEM_K8(1);
+        STEM_RD8(3);
+        STEM_K8(2);
+        STEM_K8(3);
+#undef STEM_RD8
+#undef STEM_K8
+      } else {
+        v4i fa[3], fw[3];
+#define STEM_RD(kk)                                                                                    \
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[(kk) % 3]) : "v"(ra[(kk) >> 1]), "n"(32 * ((kk) & 1)) \
+               : "memory");                                                                          \
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fw[(kk) % 3]) : "v"(w_row), "n"(32 * (kk)) : "memory")
+#define STEM_K(kk)                                                                                     \
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(fa[(kk) % 3]), "+v"(fw[(kk) % 3]) : "n"((kk) + 1 < 8 ? 2 : 0)    \
+               : "memory");                                                                          \
+  acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[(kk) % 3], fw[(kk) % 3], acc, 0, 0, 0)
+        STEM_RD(0);
+        STEM_RD(1);
+        STEM_K(0);
+        STEM_RD(2);
+        STEM_K(1);
+        STEM_RD(3);
+        STEM_K(2);
+        STEM_RD(4);
+        STEM_K(3);
+        STEM_RD(5);
+        STEM_K(4);
+        STEM_RD(6);
+        STEM_K(5);
+        STEM_RD(7);
+        STEM_K(6);
+        STEM_K(7);
+#undef STEM_RD
+#undef STEM_K
       }
       return acc;
     };
@@ -226,21 +258,19 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
       H[7] = mx3(c[14], c[15], __builtin_bit_cast(Pv, c16));
     };
 
-    // ---- prologue: pairs 0 .. SLA in flight (the ring's SLA+1 slots);
-    // convert pairs 0..2 (super rows 2py0-3 .. 2py0+2) once landed, then
-    // issue pairs SLA+1, SLA+2 into the freed slots; H of conv row 2py0-1.
-    for (int k = 0; k <= SLA; ++k) issue_pair(k);
-    if (D == 2)
-      wait_vm_const<2 * (SLA - 2)>();
-    else
-      wait_vm_const<SLA - 2>();
+    // ---- prologue: pairs 0..2 converted (super rows 2py0-3 .. 2py0+2),
+    // pairs 3 .. 2+PD loaded; H of conv row 2py0-1.
+    static_assert(PD == 2, "prologue ring assignment below assumes 3 register sets");
+    load_pair(0, raw[0]);
+    load_pair(1, raw[1]);
+    load_pair(2, raw[2]);
+    convert_pair(0, raw[0]);
+    load_pair(3, raw[0]);
+    convert_pair(1, raw[1]);
+    load_pair(4, raw[1]);
+    convert_pair(2, raw[2]);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): patch rows written (loads stay in flight)
     __builtin_amdgcn_s_barrier();
-    convert_pair(0);
-    convert_pair(1);
-    convert_pair(2);
-    __syncthreads();
-    issue_pair(SLA + 1);
-    issue_pair(SLA + 2);
     Pv Hp[8];
     if (py0 == 0) {
 #pragma unroll
@@ -257,20 +287,20 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
       const v4i o = *(const v4i*)(stg + pxl * 32 + hf * 16);
       if (lane < 28) *(v4i*)(a.y + (((size_t)n * 56 + p) * 56 + 14 * q + pxl) * 64 + ot * 32 + hf * 16) = o;
     };
-    for (int p = py0; p < py1; ++p) {
-      const int t = p - py0;
-      // Pair t+3 (super rows 2p+3, 2p+4) has landed once only the younger VM
-      // ops remain: pairs t+4 .. t+2+SLA and the stores issued in steps
-      // t-SLA+1 .. t-1 (each step stores the previous step's row before it
-      // issues its pair): min(t-1, SLA-1) of them.
+    // step t (pooled row p = py0 + t): pair t+3 (register set (t+3) % 3 =
+    // t % 3) is quantised for the next step, pair t+5 is loaded into the set
+    // pair t+2 freed, conv rows 2p and 2p+1 are computed and pooled.
+    auto step = [&](int t, auto setc) {
+      constexpr int S = decltype(setc)::value;  // == t % 3
+      const int p = py0 + t;
       ST(5);
-      wait_vm((SLA - 1) * D + (t < 1 ? 0 : (t - 1 < SLA - 1 ? t - 1 : SLA - 1)));
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): last step's patch rows and staging
       __builtin_amdgcn_s_barrier();
       ST(0);
-      convert_pair(t + 3);
+      convert_pair(t + 3, raw[S]);
       ST(1);
       if (t > 0) store_row(p - 1);
-      issue_pair(t + 3 + SLA);
+      load_pair(t + 5, raw[(S + 2) % 3]);
       ST(2);
 
       Pv He[8], Ho[8];
@@ -293,7 +323,16 @@ __global__ __launch_bounds__(SNW * 64, 1) void stem_fused_kernel(StemArgs a) {
       // 14 pooled columns x 32 channels = 28 x 16 B, staged in LDS (written by
       // this wave: LDS is in order); stored during the next step
       ST(4);
+    };
+    const int nsteps = py1 - py0;
+    int t = 0;
+    for (; t + 3 <= nsteps; t += 3) {
+      step(t, std::integral_constant<int, 0>{});
+      step(t + 1, std::integral_constant<int, 1>{});
+      step(t + 2, std::integral_constant<int, 2>{});
     }
+    if (t < nsteps) step(t, std::integral_constant<int, 0>{});
+    if (t + 1 < nsteps) step(t + 1, std::integral_constant<int, 1>{});
     if (py1 > py0) store_row(py1 - 1);
     wait_vm0();
     __syncthreads();  // ring reuse by the next item
@@ -361,16 +400,16 @@ void pack_stem_weights_f8(const uint8_t* q, const float* alpha, uint8_t* out, fl
 hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float* alpha, const float* beta,
                              float inv_s, int8_t* y, hipStream_t s, bool f8) {
   const int ncu = num_cus_stem();
-  int nb = (ncu + N - 1) / N;  // bands per image so that every CU gets an item
+  int nb = (2 * ncu + N - 1) / N;  // bands per image so that every CU gets two co-resident items
   nb = nb < 1 ? 1 : (nb > 14 ? 14 : nb);
   const int R = (56 + nb - 1) / nb;
   nb = (56 + R - 1) / R;
   StemArgs a{x, w, alpha, beta, y, inv_s, N, nb, R};
-  const int items = N * nb;
+  const int items = N * nb, grid = items < 2 * ncu ? items : 2 * ncu;
   if (f8)
-    hipLaunchKernelGGL(stem_fused_kernel<true>, dim3(items < ncu ? items : ncu), dim3(SNW * 64), 0, s, a);
+    hipLaunchKernelGGL(stem_fused_kernel<true>, dim3(grid), dim3(SNW * 64), 0, s, a);
   else
-    hipLaunchKernelGGL(stem_fused_kernel<false>, dim3(items < ncu ? items : ncu), dim3(SNW * 64), 0, s, a);
+    hipLaunchKernelGGL(stem_fused_kernel<false>, dim3(grid), dim3(SNW * 64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -56,12 +56,14 @@ def test_quantize_f32_s8(gpu):
 
 @pytest.mark.parametrize("M,N,K", [(100, 77, 61), (1000, 1, 512), (64, 3136, 576), (33, 65, 1), (256, 256, 64),
                                    (512, 768, 1152), (257, 263, 2304), (300, 520, 72), (128, 196, 4608),
-                                   (1, 5000, 3), (513, 255, 65)])
+                                   (1, 5000, 3), (513, 255, 65), (257, 272, 2304), (300, 528, 80), (33, 16, 16),
+                                   (1024, 512, 192)])
 def test_gemm_s8s8s32_reference_layout(gpu, M, N, K):
     """sgemm_tiled's layout and contract (any M, N, K) in int8 -> int32:
-    whole 256 x 256 tiles, M / N / K tails inside a tile and a stage,
-    unaligned rows (K % 16, N % 8 != 0: the byte-load path) and the extremes
-    -128 / 127, bit-exact with the oracle."""
+    whole 256 x 256 tiles, M / N / K tails inside a tile and a stage, both
+    kernels (K % 16 == N % 16 == 0: the LDS-DMA ring with transposed B reads;
+    otherwise the register-staged kernel, byte loads for unaligned rows) and
+    the extremes -128 / 127, bit-exact with the oracle."""
     from dlq_amd.lib import lib
     rng = np.random.default_rng(M + N + K)
     A = rand_s8(rng, (M, K), lo=-128)
