@@ -41,6 +41,20 @@ namespace {
 __device__ __attribute__((aligned(64))) int8_t g_trash_s2i[1024];
 __device__ __attribute__((aligned(64))) int8_t g_zero_s2i[64];
 
+// Cycle stamps for tools/probe/conv3x3s2i_probe.hip -DDLQ_STAMPS (compiled out of the library).
+#ifdef DLQ_STAMPS
+__device__ unsigned long long g_stamps_j[1024 * 8 * 64];
+#define JSTAMP(i)                                                                                  \
+  do {                                                                                             \
+    if ((threadIdx.x & 63) == 0 && (i) < 64)                                                       \
+      g_stamps_j[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define JSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
 constexpr int JL = 196;               // output pixels per item
 constexpr int JSC = 32;               // input channels per stage
 constexpr int JWP = 9 * JSC + 16;     // conv1 weight row pitch (304 B)
@@ -266,18 +280,25 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
       glds16_asm(src, lds32 + pc * 1024);
     }
   }
+  JSTAMP(0);
   prep_for(0);
+  JSTAMP(55);
 #pragma unroll
   for (int k = 0; k < DPW; ++k) issue_piece(0, k);
+  JSTAMP(56);
   init();  // published by stage 0's barrier
+  JSTAMP(57);
 
   for (int s = 0; s < nst; ++s) {
     const int li = s / NS, j = s - li * NS;
+    if (s == 0) JSTAMP(58);
     if (j == 0 && s > 0)
       wait_vm_const<STORES>();
     else
       wait_vm_const<0>();
+    if (s == 0) JSTAMP(59);
     __builtin_amdgcn_s_barrier();
+    JSTAMP(1 + 2 * s);
     const bool more = s + 1 < nst;
     if (more) prep_for(s + 1);
     if (j == 0) {
@@ -397,6 +418,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     }
     }  // int8 MFMA loop
 
+    JSTAMP(2 + 2 * s);
     if (j != NS - 1 || DLQ_ABL(a, 4)) continue;  // probe builds: timing without the epilogues
     // ---- fused epilogues of the item ----
     if constexpr (OUT == 2) {
@@ -456,7 +478,9 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
       if constexpr (DS) epi(accd, 2 * OC * 4, LO, y_ds);
     }
   }
+  JSTAMP(62);
   wait_vm0();
+  JSTAMP(63);
 }
 
 // OUT: 0 = int8 (fused epilogues), 2 = int32 conv1 accumulators (DS = false).

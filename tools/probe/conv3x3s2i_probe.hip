@@ -1,6 +1,8 @@
 // Timing probe (not product code): the 196-px stride-2 conv + fused
 // downsample kernel (conv3x3s2i.hip) on the three ResNet-18 shapes, random
 // int8 data, B = 256; argv: OW (28/14/7), dbg bits (2 = no LDS-DMA).
+// With -DDLQ_STAMPS it also prints per-wave s_memtime stamps (prologue,
+// per-stage barrier wait / MFMA loop, epilogues) of three workgroups.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //          -I dlq_amd/csrc tools/probe/conv3x3s2i_probe.hip -o tools/probe/conv3x3s2i_probe
 #define DLQ_ABLATION 1  // the kernel honours a.dbg (timing ablations)
@@ -50,5 +52,21 @@ int main(int argc, char** argv) {
   }
   float ms; hipEventElapsedTime(&ms, e0, e1);
   printf("OW=%d dbg=%d kernel %.1f us\n", OW, dbg, ms * 1e3 / 20);
+#ifdef DLQ_STAMPS
+  // per wave: prologue | per stage (barrier wait)/(MFMA loop) | epilogue, drain
+  std::vector<unsigned long long> st(1024 * 8 * 64);
+  if (hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_stamps_j), st.size() * 8) != hipSuccess) return 2;
+  const int NS = C / 32, nst = (OW == 28 ? 4 : OW == 14 ? 2 : 1) * NS;
+  for (int blk : {0, 77, 200}) {
+    for (int wv : {0, 4, 5}) {
+      const unsigned long long* s = &st[(blk * 8 + wv) * 64];
+      printf("blk %3d wave %d: pro %5llu (prep %llu issue %llu init %llu ->loop %llu vmwait %llu barrier %llu) |", blk, wv,
+             s[1] - s[0], s[55] - s[0], s[56] - s[55], s[57] - s[56], s[58] - s[57], s[59] - s[58], s[1] - s[59]);
+      for (int k = 0; k < nst; ++k)
+        printf(" %llu/%llu", k ? s[1 + 2 * k] - s[2 * k] : 0ull, s[2 + 2 * k] - s[1 + 2 * k]);
+      printf(" | tail %llu drain %llu total %llu\n", s[62] - s[2 * nst], s[63] - s[62], s[63] - s[0]);
+    }
+  }
+#endif
   return 0;
 }
