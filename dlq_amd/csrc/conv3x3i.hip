@@ -40,7 +40,7 @@ namespace dlq {
 namespace {
 
 __device__ __attribute__((aligned(64))) int8_t g_trash_i[1024];  // sink for stores past the last pixel
-__device__ __attribute__((aligned(64))) int8_t g_zero_i[64];     // DMA source of the zero halo units
+__device__ __attribute__((aligned(64))) int8_t g_zero_i[1024];   // DMA source of the zero halo units (+ j * 32 per slice)
 
 // Cycle stamps for tools/probe/conv3x3i_stamps.hip (compiled out of the library).
 #ifdef DLQ_STAMPS
@@ -130,12 +130,14 @@ __device__ __forceinline__ void conv3x3i_init(const ConvArgs& a, int8_t* lds) {
     ((int*)(lds + G::OFF_Z))[i] = 0;
     ((int*)(lds + G::SLOT + G::OFF_Z))[i] = 0;
   }
+#ifndef DLQ_X_LATEAB
   if constexpr (OUT == 0) {
     for (int i = tid; i < a.OCp; i += INW * 64) {
       ((float*)(lds + G::OFF_AB))[i] = a.alpha[i];
       ((float*)(lds + G::OFF_AB))[C + i] = a.beta[i];
     }
   }
+#endif
 }
 
 template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false>
@@ -164,61 +166,51 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     p0 = (it / n_ot) * IL;
   };
 
-  // ---- DMA issue side: pieces pc = wave + 8k; per lane the slice-0 source
-  // offset (weights: byte offset into a.w; patch: into a.x, -1 = zero unit).
-  int doff[DPW];
+  // ---- DMA plan.  A stage's pieces are PP patch pieces (per-lane sources:
+  // the item's rows; halo units read a zero block) and WP weight pieces (1 KiB
+  // blocks of the packed image: a wave-uniform base + 16 * lane, the saddr
+  // form).  Loader wave lrank issues pieces lrank + NLD k, patch pieces first;
+  // every piece's kind is wave-uniform (a scalar branch, no exec masking) and
+  // its LDS destination a constant offset in the slot (weights, then patch).
+  constexpr int KP = (G::PP + NLD - 1) / NLD;  // k < KP: possibly a patch piece
+  const int wv = __builtin_amdgcn_readfirstlane(lrank);
+  const int8_t* pptr[KP];  // this wave's patch-piece sources for slice 0 (per item)
+  const int8_t* wbase = a.w;  // the issuing item's weight blocks (wave-uniform)
   int iss_li = -1;
-  // CUs of one XCD start their piece sequence at different pieces, so they do
-  // not all request the same weight lines of the shared L2 at once (measured
-  // 1-3 % faster than every CU issuing in the same order)
-  const int rot = (int)((blockIdx.x >> 3) % DPW);
-  auto piece_of = [&](int k) {
-    int kk = k + rot;
-    kk = kk >= DPW ? kk - DPW : kk;
-    const int pc = lrank + kk * NLD;
-    return pc >= G::NPIECE ? pc - G::NPIECE : pc;  // past the end: re-issue an earlier piece
-  };
   auto prep_issue = [&](int li) {
-    // lane is made opaque here so the compiler recomputes the per-piece lane
-    // decompositions (a few VALU ops per item) instead of hoisting them out
-    // of the stage loop: hoisted, they were spilled to scratch and reloaded
-    // as ~28 serialised scratch_load + s_waitcnt vmcnt(0) at every item change
-    int lane = threadIdx.x & 63;
-    asm volatile("" : "+v"(lane));
     int ot, p0;
     item_of(li, ot, p0);
+    // weight block [ot128][j][128][304]; a 64-oc item is half of one
+    const int o128 = (ot * G::OT) >> 7, ohalf = (ot * G::OT) & 127;
+    wbase = a.w + (size_t)(o128 * NS * 128 + ohalf) * IPITCH;
     const int R0 = p0 / W;  // first global output row of the item
 #pragma unroll
-    for (int k = 0; k < DPW; ++k) {
-      const int pc = piece_of(k);
-      if (pc < G::WP) {
-        // weight block [ot128][j][128][304]; a 64-oc item is half of one
-        const int o128 = (ot * G::OT) >> 7, ohalf = (ot * G::OT) & 127;
-        doff[k] = (o128 * NS * 128 + ohalf) * IPITCH + pc * 1024 + lane * 16;
-      } else {
-        const int u = (pc - G::WP) * 64 + lane;
-        const int plane = u >= G::UP ? 1 : 0, q = u - plane * G::UP;
-        const int c = q / G::CS, rem = q - c * G::CS;
-        const int r = rem / G::RW, iw = rem - r * G::RW;
-        const int gr = R0 + c * G::RPI;  // chunk's first global output row
-        const int n = gr / H, ih = gr - n * H + r - 1;
-        const bool ok = u < 2 * G::UP && c < G::IPI && r < G::RPI + 2 && n < a.N && (unsigned)ih < (unsigned)H &&
-                        (unsigned)iw < (unsigned)W;
-        doff[k] = ok ? ((n * H + ih) * W + iw) * C + plane * 16 : -1;
-      }
+    for (int k = 0; k < KP; ++k) {
+      const int u = (wv + k * NLD) * 64 + lane;
+      const int plane = u >= G::UP ? 1 : 0, q = u - plane * G::UP;
+      const int c = q / G::CS, rem = q - c * G::CS;
+      const int r = rem / G::RW, iw = rem - r * G::RW;
+      const int gr = R0 + c * G::RPI;  // chunk's first global output row
+      const int n = gr / H, ih = gr - n * H + r - 1;
+      const bool ok = u < 2 * G::UP && c < G::IPI && r < G::RPI + 2 && n < a.N && (unsigned)ih < (unsigned)H &&
+                      (unsigned)iw < (unsigned)W;
+      // zero units: a 1 KiB zero block (slice j adds j * 32 and stays inside it)
+      pptr[k] = ok ? a.x + (size_t)(((n * H + ih) * W + iw) * C + plane * 16) : g_zero_i + (lane & 3) * 16;
     }
   };
-  auto issue_piece = [&](int s, int k) {
-    const int sc = s < nst ? s : nst - 1;
-    const int j = sc % NS;
-    const int pc = piece_of(k);
-    const int8_t* src = pc < G::WP ? a.w + (size_t)(doff[k] + j * 128 * IPITCH)
-                                   : (doff[k] < 0 ? g_zero_i + (lane & 3) * 16 : a.x + (size_t)(doff[k] + j * ISC));
-    glds16_asm(src, lds32 + (s & 1) * G::SLOT + pc * 1024);
+  auto issue_piece = [&](int s, int k) {  // s < nst
+    const int j = s % NS;
+    const int pc = wv + k * NLD;
+    const unsigned slot = lds32 + (s & 1) * G::SLOT;
+    if (k < KP && pc < G::PP) {
+      glds16_asm(pptr[k < KP ? k : 0] + j * ISC, slot + G::WB + pc * 1024);
+    } else if (pc < G::PP + G::WP) {
+      const int wp = pc - G::PP;
+      glds16_saddr(wbase + (size_t)j * 128 * IPITCH + wp * 1024, (unsigned)lane * 16, slot + wp * 1024);
+    }
   };
   auto prep_for = [&](int s) {
-    const int sc = s < nst ? s : nst - 1;
-    const int li = sc / NS;
+    const int li = s / NS;
     if (li != iss_li) {
       prep_issue(li);
       iss_li = li;
@@ -257,6 +249,16 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   }
   conv3x3i_init<W, C, OUT>(a, lds);
 
+#ifdef DLQ_X_LATEAB
+  // alpha/beta (read only by the epilogue): loaded during stage 0 (their
+  // latency no longer holds up the first barrier), written to LDS before
+  // stage 1's barrier, which publishes them
+  static_assert(C <= INW * 64, "one alpha/beta per thread");
+  float ab_al = 0.f, ab_be = 0.f;
+#endif
+#ifdef DLQ_X_PRIO
+  if (threadIdx.x >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
   for (int s = 0; s < nst; ++s) {
     const int li = s / NS, j = s - li * NS;
     // Stage s has landed once every older VM op is done except the previous
@@ -265,7 +267,23 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       wait_vm_const<STORES>();
     else
       wait_vm_const<0>();
+#ifdef DLQ_X_LATEAB
+    if constexpr (OUT == 0) {
+      if (s == 1 && tid < a.OCp) {
+        ((float*)(lds + G::OFF_AB))[tid] = ab_al;
+        ((float*)(lds + G::OFF_AB))[C + tid] = ab_be;
+      }
+    }
+#endif
     __builtin_amdgcn_s_barrier();
+#ifdef DLQ_X_LATEAB
+    if constexpr (OUT == 0) {
+      if (s == 0 && tid < a.OCp) {
+        ab_al = a.alpha[tid];
+        ab_be = a.beta[tid];
+      }
+    }
+#endif
     ISTAMP(1 + 2 * s);
     const bool more = s + 1 < nst;
     if (more && loader) prep_for(s + 1);
@@ -309,6 +327,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       fa2[0] = ld_a2(0);
 #pragma unroll
       for (int i = 0; i < D; ++i) fbr[i] = ld_b2(i);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int pr = 0; pr < NPAIR; ++pr) {
         if (pr + 1 < NPAIR) fa2[(pr + 1) & 1] = ld_a2(pr + 1);
@@ -342,6 +361,9 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     fa[0] = *(const v4i*)abase;
 #pragma unroll
     for (int f = 0; f < NF; ++f) ld_b(0, f);
+    // keep tap 0's fragment reads here: left to the scheduler they were sunk
+    // into tap 0's MFMA slots and serialised (one lgkmcnt(0) per MFMA)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int bu = tap & 1;

@@ -39,7 +39,7 @@ namespace dlq {
 namespace {
 
 __device__ __attribute__((aligned(64))) int8_t g_trash_s2i[1024];
-__device__ __attribute__((aligned(64))) int8_t g_zero_s2i[64];
+__device__ __attribute__((aligned(64))) int8_t g_zero_s2i[1024];  // zero halo source (+ j * 32 per slice)
 
 // Cycle stamps for tools/probe/conv3x3s2i_probe.hip -DDLQ_STAMPS (compiled out of the library).
 #ifdef DLQ_STAMPS
@@ -171,63 +171,54 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     p0 = (it / n_ot) * JL;
   };
 
-  // ---- DMA issue side (pieces pc = wave + 8k): conv weights, ds weights, patch
-  int doff[DPW];
+  // ---- DMA plan (as in conv3x3i.hip): PP patch pieces (per-lane sources,
+  // halo units from a zero block) then WPC weight pieces (conv block, then
+  // downsample block: a wave-uniform base + 16 * lane, the saddr form); wave
+  // w issues pieces w + 8k, each of wave-uniform kind, to a constant offset
+  // in the slot.
+  constexpr int KP = (G::PP + JNW - 1) / JNW;  // k < KP: possibly a patch piece
+  constexpr int WCP = G::WB / 1024;            // conv weight pieces (then ds pieces)
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int8_t* pptr[KP];
+  const int8_t* wb_c = a.w;   // the issuing item's conv / downsample weight blocks (wave-uniform)
+  const int8_t* wb_d = w_ds;
   int iss_li = -1;
-  const int rot = (int)((blockIdx.x >> 3) % DPW);  // stagger the XCD's CUs over the shared weight lines
-  auto piece_of = [&](int k) {
-    int kk = k + rot;
-    kk = kk >= DPW ? kk - DPW : kk;
-    const int pc = wave + kk * JNW;
-    return pc >= G::NPIECE ? pc - G::NPIECE : pc;
-  };
   auto prep_issue = [&](int li) {
-    // lane is made opaque here so the compiler recomputes the per-piece lane
-    // decompositions (a few VALU ops per item) instead of hoisting them out
-    // of the stage loop: hoisted, they were spilled to scratch and reloaded
-    // as ~28 serialised scratch_load + s_waitcnt vmcnt(0) at every item change
-    int lane = threadIdx.x & 63;
-    asm volatile("" : "+v"(lane));
     int ot, p0;
     item_of(li, ot, p0);
+    wb_c = a.w + (size_t)ot * NS * G::WB;
+    if constexpr (DS) wb_d = w_ds + (size_t)ot * NS * G::DB;
     const int R0 = p0 / OW;  // first global output row
 #pragma unroll
-    for (int k = 0; k < DPW; ++k) {
-      const int pc = piece_of(k);
-      if (pc < G::WPC && pc < G::WB / 1024) {
-        doff[k] = ot * NS * G::WB + pc * 1024 + lane * 16;
-      } else if (pc < G::WPC) {
-        doff[k] = ot * NS * G::DB + (pc - G::WB / 1024) * 1024 + lane * 16;
-      } else {
-        const int u = (pc - G::WPC) * 64 + lane;
-        const int plane = u >= G::UP ? 1 : 0, q = u - plane * G::UP;
-        const int c = q / G::CS, rem = q - c * G::CS;
-        const int r = rem / G::WI, pos = rem - r * G::WI;
-        const int iw = pos < OW ? 2 * pos : 2 * (pos - OW) + 1;  // de-interleaved: even cols, then odd
-        const int gr = R0 + c * G::RPI;  // chunk's first global output row
-        const int n = gr / G::OH, ih = 2 * (gr - n * G::OH) - 1 + r;
-        const bool ok = u < 2 * G::UP && c < G::IPI && r < G::IRC && n < a.N && (unsigned)ih < (unsigned)G::HI;
-        doff[k] = ok ? ((n * G::HI + ih) * G::WI + iw) * C + plane * 16 : -1;
-      }
+    for (int k = 0; k < KP; ++k) {
+      const int u = (wv + k * JNW) * 64 + lane;
+      const int plane = u >= G::UP ? 1 : 0, q = u - plane * G::UP;
+      const int c = q / G::CS, rem = q - c * G::CS;
+      const int r = rem / G::WI, pos = rem - r * G::WI;
+      const int iw = pos < OW ? 2 * pos : 2 * (pos - OW) + 1;  // de-interleaved: even cols, then odd
+      const int gr = R0 + c * G::RPI;  // chunk's first global output row
+      const int n = gr / G::OH, ih = 2 * (gr - n * G::OH) - 1 + r;
+      const bool ok = u < 2 * G::UP && c < G::IPI && r < G::IRC && n < a.N && (unsigned)ih < (unsigned)G::HI;
+      // zero units: a 1 KiB zero block (slice j adds j * 32 and stays inside it)
+      pptr[k] = ok ? a.x + (size_t)(((n * G::HI + ih) * G::WI + iw) * C + plane * 16) : g_zero_s2i + (lane & 3) * 16;
     }
   };
-  auto issue_piece = [&](int s, int k) {
-    const int sc = s < nst ? s : nst - 1;
-    const int j = sc % NS;
-    const int pc = piece_of(k);
-    const int8_t* src;
-    if (pc < G::WPC && pc < G::WB / 1024)
-      src = a.w + (size_t)(doff[k] + j * G::WB);
-    else if (pc < G::WPC)
-      src = w_ds + (size_t)(doff[k] + j * G::DB);
-    else
-      src = doff[k] < 0 ? g_zero_s2i + (lane & 3) * 16 : a.x + (size_t)(doff[k] + j * JSC);
-    const int dst = pc < G::WPC ? pc * 1024 : G::OFF_P + (pc - G::WPC) * 1024;
-    glds16_asm(src, lds32 + (s & 1) * G::SLOT + dst);
+  auto issue_piece = [&](int s, int k) {  // s < nst
+    const int j = s % NS;
+    const int pc = wv + k * JNW;
+    const unsigned slot = lds32 + (s & 1) * G::SLOT;
+    if (k < KP && pc < G::PP) {
+      glds16_asm(pptr[k < KP ? k : 0] + j * JSC, slot + G::OFF_P + pc * 1024);
+    } else if (pc < G::PP + G::WPC) {
+      const int wp = pc - G::PP;
+      if (wp < WCP)
+        glds16_saddr(wb_c + (size_t)j * G::WB + wp * 1024, (unsigned)lane * 16, slot + wp * 1024);
+      else
+        glds16_saddr(wb_d + (size_t)j * G::DB + (wp - WCP) * 1024, (unsigned)lane * 16, slot + wp * 1024);
+    }
   };
   auto prep_for = [&](int s) {
-    const int sc = s < nst ? s : nst - 1;
-    const int li = sc / NS;
+    const int li = s / NS;
     if (li != iss_li) {
       prep_issue(li);
       iss_li = li;
@@ -255,6 +246,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
 
   auto init = [&]() {  // LDS constants after the first DMA issue: their load latency overlaps it
     const int t = threadIdx.x;
+#ifndef DLQ_X_LATEAB
     if constexpr (OUT == 0) {
       float* ab = (float*)(lds + G::OFF_AB);
       for (int i = t; i < a.OCp; i += JNW * 64) {
@@ -266,6 +258,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
         }
       }
     }
+#endif
     for (int i = t; i < G::ZU * 4; i += JNW * 64) {
       ((int*)(lds + G::OFF_Z))[i] = 0;
       ((int*)(lds + G::SLOT + G::OFF_Z))[i] = 0;
@@ -289,6 +282,15 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
   init();  // published by stage 0's barrier
   JSTAMP(57);
 
+#ifdef DLQ_X_LATEAB
+  // alpha/beta (read only by the epilogues): loaded during stage 0, written to
+  // LDS before stage 1's barrier (NS >= 2), which publishes them
+  static_assert(OC <= JNW * 64, "one alpha/beta per thread");
+  float ab_v[DS ? 4 : 2] = {};
+#endif
+#ifdef DLQ_X_PRIO
+  if (threadIdx.x >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
   for (int s = 0; s < nst; ++s) {
     const int li = s / NS, j = s - li * NS;
     if (s == 0) JSTAMP(58);
@@ -297,7 +299,32 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     else
       wait_vm_const<0>();
     if (s == 0) JSTAMP(59);
+#ifdef DLQ_X_LATEAB
+    if constexpr (OUT == 0) {
+      if (s == 1 && tid < a.OCp) {
+        float* ab = (float*)(lds + G::OFF_AB);
+        ab[tid] = ab_v[0];
+        ab[OC + tid] = ab_v[1];
+        if constexpr (DS) {
+          ab[2 * OC + tid] = ab_v[2];
+          ab[3 * OC + tid] = ab_v[3];
+        }
+      }
+    }
+#endif
     __builtin_amdgcn_s_barrier();
+#ifdef DLQ_X_LATEAB
+    if constexpr (OUT == 0) {
+      if (s == 0 && tid < a.OCp) {
+        ab_v[0] = a.alpha[tid];
+        ab_v[1] = a.beta[tid];
+        if constexpr (DS) {
+          ab_v[2] = al_ds[tid];
+          ab_v[3] = be_ds[tid];
+        }
+      }
+    }
+#endif
     JSTAMP(1 + 2 * s);
     const bool more = s + 1 < nst;
     if (more) prep_for(s + 1);
@@ -342,6 +369,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
       fa2[0] = ld_a2(0);
 #pragma unroll
       for (int i = 0; i < D; ++i) fbr[i] = ld_b2(i);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int pr = 0; pr < NPAIR; ++pr) {
         if (pr + 1 < NPAIR) fa2[(pr + 1) & 1] = ld_a2(pr + 1);
@@ -374,6 +402,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     fa[0] = *(const v4i*)abase;
 #pragma unroll
     for (int f = 0; f < NF; ++f) ld_b(0, f);
+    __builtin_amdgcn_sched_barrier(0);  // tap 0's fragment reads stay here (see conv3x3i.hip)
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int bu = tap & 1;

@@ -138,6 +138,14 @@ __device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_addr) 
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "{m0}"(m0) : "memory");
 }
 
+// One LDS-DMA piece whose 64 sources are a wave-uniform base + a per-lane
+// 32-bit offset (the saddr form: base in an SGPR pair, computed by the
+// compiler in 64-bit pointer arithmetic from uniform values).
+__device__ __forceinline__ void glds16_saddr(const void* base, unsigned voff, unsigned lds_addr) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(base), "{m0}"(m0) : "memory");
+}
+
 // LDS byte address of a __shared__ pointer (for M0).
 __device__ __forceinline__ unsigned lds_addr32(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;

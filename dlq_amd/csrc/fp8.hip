@@ -397,7 +397,7 @@ int dlq_conv2d_s2_ds_nhwc_f8(const dlq_conv_desc* d, const uint8_t* x, const uin
     return fail(DLQ_ERR_ARG, "conv2d_s2_ds_f8: needs a 3x3/s2/p1 C->2C conv at 56x56x64, 28x28x128 or 14x14x256");
   if (!alpha || !beta || !w_ds || !alpha_ds || !beta_ds || !y_ds)
     return fail(DLQ_ERR_ARG, "conv2d_s2_ds_f8: null pointer");
-  if (!f8_wide(F8_GEOM(d))) return fail(DLQ_ERR_STATE, "conv2d_s2_ds_f8: disabled by DLQ_F8_GENERIC");
+  if (!f8_wide(F8_GEOM(d))) return fail(DLQ_ERR_STATE, "conv2d_s2_ds_f8: shape not supported by the fused fp8 stride-2 kernel");
   ConvArgs a;
   int rc = conv_args_checked(d, (const int8_t*)x, (const int8_t*)w_packed, alpha, beta, nullptr, 0.f, 1, DLQ_OUT_S8,
                              y, a);

@@ -226,6 +226,9 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_kernel(const int8_t* __re
     const int younger = nst - 1 - s < 2 ? nst - 1 - s : 2;  // stages issued after s (4 pieces each)
     wait_vm(4 * younger);
     __builtin_amdgcn_s_barrier();
+    // the waitcnt and barrier builtins are not memory operations to the
+    // compiler: this keeps the slot's fragment reads below them
+    asm volatile("" ::: "memory");
     if (s + 3 < nst) issue(s + 3);  // into the slot stage s - 1 left
     const int8_t* la = lds + (s % GSLOTS) * GSLOT_DMA;
     const int8_t* lb = la + GSLOT_A;

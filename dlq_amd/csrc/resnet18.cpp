@@ -1222,7 +1222,11 @@ struct DevArena {  // per-call device allocations, freed on scope exit
   int upload(T** out, const T* src, size_t n, hipStream_t s) {
     int rc = alloc(out, n * sizeof(T));
     if (rc) return rc;
+    // synchronous (on the stream): the host vectors behind src are
+    // temporaries of the caller, and a pageable async copy is not guaranteed
+    // to have staged them when the call returns
     hipError_t e = hipMemcpyAsync(*out, src, n * sizeof(T), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
     return e == hipSuccess ? DLQ_OK : hip_fail(e, "fp32 weight upload");
   }
 };

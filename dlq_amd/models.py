@@ -210,6 +210,8 @@ class ResNet18Int8:
         """Set every activation scale from the GPU fp32 reference forward over
         x (dlq_resnet18_calibrate) and prepare again."""
         from .lib import stream_handle
+        if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.shape[1:] == (3, 224, 224)):
+            raise TypeError("x must be a contiguous CUDA fp32 [B,3,224,224] tensor")
         self._check(self._lib.dlq_resnet18_calibrate(self.h, x.data_ptr(), x.shape[0], float(qmax), stream_handle()),
                     "resnet18_calibrate")
         self._check(self._lib.dlq_resnet18_prepare(self.h, self.max_batch, None), "resnet18_prepare")

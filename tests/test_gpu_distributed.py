@@ -96,3 +96,57 @@ def test_dp_world2_engine_gather(gpu, per):
         from oracle import oracle as O
         want, _ = O.resnet18_forward_s8(sd, scales, x_all.cpu().numpy())
         assert np.array_equal(ref.view(np.int32), want.view(np.int32))
+
+
+def _worker8(rank, world, port, per, sd, scales, q):
+    """One rank of BASELINE configs[3] on the box's one GPU: its own 256-image
+    shard (seed 4000 + rank), the engine through bench.GatherPipeline."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from dlq_amd.models import ResNet18Int8, synthetic_images
+        torch.cuda.set_device(0)
+        x_local = synthetic_images(per, seed=4000 + rank).cuda().contiguous()
+        model = ResNet18Int8(sd, scales, max_batch=per)
+        dev_logits = torch.empty((per, 1000), dtype=torch.float32, device="cuda")
+
+        def fwd_into(x, out):
+            model.forward(x, dev_logits)
+            out.copy_(dev_logits.cpu())
+
+        pipe = bench.GatherPipeline(fwd_into, per, world, "cpu")
+        k = pipe.step(x_local)
+        pipe.finish()
+        loaded = any("libdlq.so" in l for l in open("/proc/self/maps"))
+        q.put((rank, pipe.out[k].numpy() if rank == 0 else None, loaded))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_world8_configs3_global_batch(gpu):
+    """BASELINE configs[3] at its workload: world 8 x 256 images = 2048
+    (gloo on the one GPU box; bench.py runs the same pipeline over RCCL on the
+    8-GPU node).  The gathered [2048, 1000] logits equal one process's B = 2048
+    forward bit for bit (anchor: the logits of infer_e2e.cu:206-219's fc_forward)."""
+    from dlq_amd.models import ResNet18Int8, synthetic_images
+    from tests.helpers import model_and_scales
+    world, per = 8, 256
+    sd, scales = model_and_scales()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker8, args=(r, world, port, per, sd, scales, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=400) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[2] for r in res), "every rank must run libdlq.so"
+    got = next(r[1] for r in res if r[0] == 0)
+    assert got.shape == (world * per, 1000)
+    x_all = torch.cat([synthetic_images(per, seed=4000 + r) for r in range(world)]).cuda()
+    ref = ResNet18Int8(sd, scales, max_batch=world * per)(x_all).cpu().numpy()
+    assert np.array_equal(got.view(np.int32), ref.view(np.int32))

@@ -78,6 +78,34 @@ def test_gemm_s8s8s32_reference_layout(gpu, M, N, K):
     assert np.array_equal(Cd.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("M,N,K,a_off,b_off", [(300, 520, 128, 0, 0), (257, 264, 2304, 0, 0), (256, 256, 64, 1, 0),
+                                               (300, 520, 128, 0, 8), (200, 512, 256, 16, 24),
+                                               (130, 264, 96, 3, 5)])
+def test_gemm_s8s8s32_kernel_selection(gpu, M, N, K, a_off, b_off):
+    """The alignment-based kernel choice of dlq_gemm_s8s8s32: K % 16 == 0 with
+    N % 8 == 0 but N % 16 != 0 (or B only 8-byte aligned) takes the
+    register-staged kernel's vector loads (uint2 B rows, 16-byte A rows);
+    offset base pointers (A = buf[a_off:], B = buf[b_off:]) move a shape
+    between the LDS-DMA kernel, the vector-load path and the byte-load path.
+    Bit-exact with the oracle in every case."""
+    from dlq_amd.lib import lib
+    rng = np.random.default_rng(M * 7 + N + K + a_off + b_off)
+    A = rand_s8(rng, (M, K), lo=-128)
+    B = rand_s8(rng, (K, N), lo=-128)
+    A.flat[:3] = -128
+    B.flat[-3:] = -128
+    ref = np.empty((M, N), np.int32)
+    O.lib().ora_gemm_s8s8s32(A, B, ref, M, N, K)
+    abuf = torch.zeros(M * K + 64, dtype=torch.int8, device="cuda")
+    bbuf = torch.zeros(K * N + 64, dtype=torch.int8, device="cuda")
+    abuf[a_off:a_off + M * K] = torch.from_numpy(A.reshape(-1)).cuda()
+    bbuf[b_off:b_off + K * N] = torch.from_numpy(B.reshape(-1)).cuda()
+    Cd = torch.empty((M, N), dtype=torch.int32, device="cuda")
+    _ok(lib.dlq_gemm_s8s8s32(abuf.data_ptr() + a_off, bbuf.data_ptr() + b_off, _p(Cd), M, N, K, None))
+    torch.cuda.synchronize()
+    assert np.array_equal(Cd.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("IC,OC,k,s,p,H,N", [(3, 64, 7, 2, 3, 224, 1), (64, 64, 3, 1, 1, 56, 2),
                                              (64, 128, 1, 2, 0, 56, 2), (128, 128, 3, 1, 1, 28, 3),
                                              (256, 512, 3, 2, 1, 14, 2)])

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Build a variant of libdlq.so for A/B timing (tools/ab.py):
+#   tools/build_variant.sh NAME "-DFLAG=1 ..."
+# -> scratch/NAME/libdlq.so (scratch/ is git-ignored; it travels to the GPU box).
+set -e
+cd "$(dirname "$0")/.."
+NAME=$1
+shift
+FLAGS="$*"
+OUT=scratch/$NAME
+mkdir -p $OUT/obj
+HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result $FLAGS"
+pids=()
+objs=()
+for f in dlq_amd/csrc/*.hip dlq_amd/csrc/*.cpp; do
+  b=$(basename $f)
+  [ "$b" = main_e2e.cpp ] && continue
+  o=$OUT/obj/${b%.*}.o
+  objs+=($o)
+  if [[ $f == *.cpp ]]; then x="-x hip"; else x=""; fi
+  /opt/rocm/bin/hipcc $HIPFLAGS $x -c -o $o $f &
+  pids+=($!)
+  if [ ${#pids[@]} -ge 8 ]; then wait ${pids[0]}; pids=("${pids[@]:1}"); fi
+done
+for p in "${pids[@]}"; do wait $p; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libdlq.so "${objs[@]}"
+echo "built $OUT/libdlq.so ($FLAGS)"

@@ -1,8 +1,7 @@
 """Per-layer conv microbenchmark (HIP-event timed) for kernel A/B work.
 
-usage: python tools/convbench.py [--batch 256] [--iters 50]
-Env: DLQ_CONV_V1=1 forces the v1 implicit-GEMM kernel; DLQ_DBG=<bits> ablates
-parts of the v2 kernel (1 MFMA, 2 LDS-DMA, 4 stores) -- timing only.
+usage: python tools/convbench.py [--batch 256] [--iters 50] [--only l2,l3,...]
+(A/B of library builds: DLQ_LIB_PATH selects the libdlq.so, tools/ab.py.)
 """
 import argparse
 import os
@@ -56,7 +55,7 @@ def main():
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     rng = np.random.default_rng(0)
-    tag = f"v1={os.environ.get('DLQ_CONV_V1', '0')} dbg={os.environ.get('DLQ_DBG', '0')}"
+    tag = os.path.basename(os.path.dirname(os.environ.get("DLQ_LIB_PATH", "dlq_amd/libdlq.so")))
     if "stemf" in args.only.split(","):
         x = torch.randn(args.batch, 3, 224, 224, device="cuda")
         q = rng.integers(-127, 128, size=(64, 3, 7, 7), dtype=np.int8)

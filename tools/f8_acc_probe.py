@@ -38,7 +38,7 @@ def emulate(x, w, s, p):
 def main():
     rng = np.random.default_rng(5)
     res = {}
-    tag = "_generic" if os.environ.get("DLQ_F8_GENERIC") == "1" else ""
+    tag = ""
     for (Cc, OC, k, s, p, H) in [(256, 128, 3, 1, 1, 14), (128, 128, 3, 1, 1, 28), (512, 128, 3, 1, 1, 7),
                                  (256, 256, 3, 1, 1, 14)]:
         x = O.quantize_f32_f8(np.abs(rng.standard_normal((1, Cc, H, H))).astype(np.float32) * 40, 1.0)
