@@ -451,6 +451,270 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
   wait_vm0();
 }
 
+// ---- int8: software-pipelined jobs -------------------------------------
+// The same phases, rings, resident weights and epilogue arithmetic as
+// block_l1_kernel, with one-tile jobs (32 oc x 32 px x 576 K: ONE
+// accumulation chain of 18 v_mfma_i32_32x32x32_i8) and the epilogue of job
+// k - 1 interleaved with the MFMA chain of job k (two accumulator sets), so a
+// wave's requantisation VALU hides in its own MFMA gaps instead of leaving
+// the SIMD's matrix pipe to the partner wave.  A phase's 14 tiles per oc half
+// are dealt by parity (tile t = par + 2k, k < 7), so every SIMD (waves w and
+// w + 4: one conv1 and one conv2 wave of the same oc half and parity) gets 7
+// conv1 and 7 conv2 jobs.  Measured before: the SIMD pairs' 4 + 3 two-tile
+// jobs left the conv1 waves 30-40 % of the phase at the barrier while the
+// conv2 waves ran their VALU-heavy residual epilogues serially.
+// Untracked fragment reads never stay in flight across a branch or a loop
+// edge (each job reads its own first two k-steps); the residual is a
+// compiler-tracked load (conv2 waves issue no LDS-DMA, so the compiler's
+// vmcnt arithmetic is exact for them).
+template <bool SECOND>
+__device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds, unsigned lds32, int wave, int rows,
+                                                 int nphase) {
+  const int lane = threadIdx.x & 63, lr = lane & 31, lh = lane >> 5;
+  const int NG = gridDim.x, b = blockIdx.x;
+  const int h = wave & 1, par = (wave >> 1) & 1;  // output-channel half, tile parity
+  v4i wr[KS];
+  const int8_t* ws = SECOND ? a.w2 : a.w1;
+  const int ol = h * 32 + lr;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int tap = ks >> 1, kk = ks & 1;
+    wr[ks] = *(const v4i*)(ws + ol * 576 + tap * 64 + (((2 * kk + lh) ^ ((ol >> 2) & 3)) << 4));
+  }
+  float al[16], be[16];
+  {
+    const float* pa = SECOND ? a.a2 : a.a1;
+    const float* pb = SECOND ? a.b2 : a.b1;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        al[4 * g4 + e] = pa[h * 32 + 8 * g4 + 4 * lh + e];
+        be[4 * g4 + e] = pb[h * 32 + 8 * g4 + 4 * lh + e];
+      }
+  }
+  auto row_src = [&](int R) -> const int8_t* {
+    if (R < 0 || R >= rows) return nullptr;
+    const int j = R / LW, r = R - j * LW;
+    return a.x + ((size_t)(b + j * NG) * LW + r) * (LW * LC);
+  };
+  const bool pix_lane = lane >= 1 && lane <= LW;
+  auto dma_piece = [&](int R, int p) {
+    const int8_t* rp = row_src(R);
+    const int8_t* src = (rp && pix_lane) ? rp + (lane - 1) * LC + p * 16 : g_zero_b + (lane & 3) * 16;
+    glds16_asm(src, lds32 + OFF_IN + p * PL + pos_mod(R, NR) * PROW);
+  };
+  for (int P = wave; P < 36; P += 8) dma_piece(P >> 2, P & 3);  // rows 0..8
+  wait_vm0();
+  __syncthreads();
+
+  auto row_addrs = [&](int ring, int s0, int r, int col, bool valid, unsigned (&ra)[3]) {
+    int sl = s0;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      if (kh) {
+        ++sl;
+        if (sl == NR) sl = 0;
+      }
+      const bool rok = valid && (kh == 0 ? r > 0 : kh == 2 ? r < LW - 1 : true);
+      ra[kh] = lds32 + ring + lh * PL + (rok ? sl : NR) * PROW + 16 * col;
+    }
+  };
+  // one epilogue group (4 values: MFMA-layout register group g4) of a finished tile
+  auto epi_group = [&](const v16i& acc, int g4, const unsigned (&rg)[4]) -> unsigned {
+    const int ac[4] = {acc[4 * g4], acc[4 * g4 + 1], acc[4 * g4 + 2], acc[4 * g4 + 3]};
+    if constexpr (SECOND)
+      return epi4_res_relu(ac, al + 4 * g4, be + 4 * g4, rg[g4], a.s_res);
+    else
+      return epi4_relu(ac, al + 4 * g4, be + 4 * g4);
+  };
+  // store layout -> MFMA layout
+  auto res_regs = [&](const v4i& rs, unsigned (&rg)[4]) {
+    unsigned rr[4] = {(unsigned)rs[0], (unsigned)rs[1], (unsigned)rs[2], (unsigned)rs[3]};
+    swap32(rr[0], rr[1]);
+    swap32(rr[2], rr[3]);
+    rg[0] = rr[0];
+    rg[1] = rr[2];
+    rg[2] = rr[1];
+    rg[3] = rr[3];
+  };
+
+  // the conv2 waves are the critical path (residual epilogues): they win
+  // the SIMD's issue arbitration against their conv1 partner, which then
+  // spends less of the phase waiting at the barrier
+#ifndef DLQ_L1_PRIOJ
+#define DLQ_L1_PRIOJ 5  // measured: 5 of 7 jobs 64.2-64.5 us, all 7 66.0, none 65.9-67.4 (tools/probe/block_l1_sp_stamps.hip)
+#endif
+  BT_DECL;
+  for (int g = 0; g < nphase; ++g) {
+    const int G = g * RPH;
+    const int S_in = pos_mod(G - 1, NR), S_mid1 = G % NR, r01 = G % LW;
+    const int S_mid2 = pos_mod(G - 10, NR), rr0 = pos_mod(G - 9, LW), jm0 = (G - 9 - rr0) / LW;
+    // this phase's jobs k = kb .. ke-1 (tile t = par + 2k; wave-uniform)
+    int kb = 0, ke = 0;
+    if constexpr (!SECOND) {
+      if (G < rows) ke = 7;
+    } else if (G - 9 >= 0 && G - 2 < rows) {  // every output row of the phase exists
+      ke = 7;
+    } else {
+      for (int k = 0; k < 7; ++k) {  // output rows G-9 + (32t .. 32t+31) / 56 must reach [0, rows)
+        const int t = par + 2 * k;
+        const int R0 = G - 9 + (t * 32) / LW, R1 = G - 9 + (t * 32 + 31) / LW;
+        const bool any = R1 >= 0 && R0 < rows;
+        if (any && ke == kb) {
+          kb = k;
+          ke = k + 1;
+        } else if (any) {
+          ke = k + 1;
+        }
+      }
+    }
+    // conv1 waves stream input rows G+9 .. G+16 (plane = wave), two pieces
+    // per job over the first four jobs
+    int dma_left = (!SECOND && G + 9 < rows) ? 8 : 0, dma_row = 0;
+    auto dma_some = [&](int n) {
+      for (int e = 0; e < n && dma_left > 0; ++e, --dma_left, ++dma_row) dma_piece(G + 9 + dma_row, wave);
+    };
+
+    // per job: tap row bases, then (conv1) the intermediate slot offset or
+    // (conv2) the residual and the output pointer
+    struct Job {
+      unsigned ra[3];
+      unsigned wa;
+      v4i rq;
+      int8_t* dst;
+    };
+    auto setup = [&](int k, Job& jb) {
+      const int t = par + 2 * k;
+      const int px = t * 32 + lr;
+      const int ro = (px * 1171) >> 16;  // px / 56 for px < 448
+      const int col = px - ro * LW;
+      if constexpr (!SECOND) {
+        int s0 = S_in + ro;
+        if (s0 >= NR) s0 -= NR;
+        row_addrs(OFF_IN, s0, r01 + ro, col, true, jb.ra);
+        int sm = S_mid1 + ro;
+        if (sm >= NR) sm -= NR;
+        jb.wa = OFF_MID + (2 * h + lh) * PL + sm * PROW + 16 * (col + 1);
+      } else {
+        const int R = G - 9 + ro;
+        const bool valid = R >= 0 && R < rows;
+        int r = rr0 + ro, jm = jm0;
+        if (r >= LW) {
+          r -= LW;
+          ++jm;
+        }
+        int s0 = S_mid2 + ro;
+        if (s0 >= NR) s0 -= NR;
+        row_addrs(OFF_MID, s0, r, col, valid, jb.ra);
+        const size_t pix = valid ? ((size_t)(b + jm * NG) * LW + r) * LW + col : 0;
+        jb.rq = *(const v4i*)(a.x + pix * LC + h * 32 + lh * 16);
+        jb.dst = valid ? a.y + pix * LC + h * 32 + lh * 16 : g_trash_b + lane * 16;
+      }
+    };
+    auto finish = [&](const v4i& o, const Job& jb) {
+      if constexpr (SECOND)
+        *(v4i*)jb.dst = o;
+      else
+        *(v4i*)(lds + jb.wa) = o;
+    };
+    v16i acc[2];
+    Job job[2];
+    // job k in set A (acc[A], job[A]); with PREV, job k-1 (set 1 - A) is
+    // requantised and stored between the chain's MFMAs
+    auto run = [&](auto ac, auto pc, int k) {
+      constexpr int A = decltype(ac)::value, E = 1 - A;
+      constexpr bool PREV = decltype(pc)::value;
+      if constexpr (SECOND) {  // the first DLQ_L1_PRIOJ jobs of a phase at priority 1
+        if (k - kb == 0) __builtin_amdgcn_s_setprio(DLQ_L1_PRIOJ > 0 ? 1 : 0);
+        if (k - kb == DLQ_L1_PRIOJ) __builtin_amdgcn_s_setprio(0);
+      }
+      setup(k, job[A]);
+      if constexpr (!SECOND) dma_some(k - kb < 4 ? 2 : 0);
+      v4i bf[3];
+      auto ld = [&](auto nc, int buf) {
+        constexpr int n = decltype(nc)::value, tap = n >> 1, kh = tap / 3, kw = tap % 3;
+        constexpr int off = 16 * kw + (n & 1) * 2 * PL;
+        bf[buf] = ds_read16<off>(job[A].ra[kh]);
+      };
+      ld(std::integral_constant<int, 0>{}, 0);
+      ld(std::integral_constant<int, 1>{}, 1);
+      unsigned rg[4] = {0, 0, 0, 0}, qv[4] = {0, 0, 0, 0};
+      acc[A] = v16i{0};
+      auto step = [&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        if constexpr (s + 2 < KS) ld(std::integral_constant<int, s + 2>{}, (s + 2) % 3);
+        if constexpr (PREV) {
+          if constexpr (SECOND && s == 1) res_regs(job[E].rq, rg);
+          if constexpr (s == 3 || s == 6 || s == 9 || s == 12) qv[(s - 3) / 3] = epi_group(acc[E], (s - 3) / 3, rg);
+          if constexpr (s == 14) finish(mfma_to_store16(qv[0], qv[1], qv[2], qv[3]), job[E]);
+        }
+        // younger LDS ops than this k-step's read: the (up to) two prefetches,
+        // plus at most one intermediate-ring write (waiting for it is harmless)
+        constexpr int young = (s + 2 < KS ? 2 : s + 1 < KS ? 1 : 0);
+        asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(bf[s % 3]) : "n"(young) : "memory");
+        acc[A] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wr[s], bf[s % 3], acc[A], 0, 0, 0);
+      };
+      static_for<0, KS>(step);
+    };
+    auto final_epi = [&](auto ac) {  // the phase's last job, after its chain
+      constexpr int A = decltype(ac)::value;
+      unsigned rg[4] = {0, 0, 0, 0}, qv[4];
+      if constexpr (SECOND) res_regs(job[A].rq, rg);
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) qv[g4] = epi_group(acc[A], g4, rg);
+      finish(mfma_to_store16(qv[0], qv[1], qv[2], qv[3]), job[A]);
+    };
+    const std::integral_constant<int, 0> I0;
+    const std::integral_constant<int, 1> I1;
+    const std::integral_constant<bool, false> NOPREV;
+    const std::integral_constant<bool, true> WPREV;
+    BT(0);
+    if (ke > kb) {
+      run(I0, NOPREV, kb);
+      int k = kb + 1;
+      for (; k + 1 < ke; k += 2) {
+        run(I1, WPREV, k);
+        run(I0, WPREV, k + 1);
+      }
+      if (k < ke) {  // an odd job left: it runs in set 1, the last epilogue is set 1's
+        run(I1, WPREV, k);
+        final_epi(I1);
+      } else {
+        final_epi(I0);
+      }
+    }
+    BT(1);
+    if constexpr (!SECOND) {
+      dma_some(8);
+      wait_vm0();  // this phase's DMA has landed
+    }
+    BT(2);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): intermediate rows written (vmcnt untouched)
+    __builtin_amdgcn_s_barrier();
+    BT(3);
+  }
+  BT_STORE();
+  wait_vm0();
+}
+
+__global__ __launch_bounds__(512, 1) void block_l1_sp_kernel(BlockArgs a) {
+  __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int NG = gridDim.x, b = blockIdx.x;
+  const int J = (a.N - b + NG - 1) / NG;  // images b, b+NG, ... of this workgroup
+  const int rows = J * LW;
+  const int nphase = rows / RPH + 2;  // conv2 trails conv1 by 9 rows
+  for (int i = tid; i < RING / 16; i += 512) *(v4i*)(lds + OFF_MID + 16 * i) = v4i{0, 0, 0, 0};
+  for (int i = tid; i < 4 * PROW / 16; i += 512)
+    *(v4i*)(lds + OFF_IN + (i >> 6) * PL + NR * PROW + 16 * (i & 63)) = v4i{0, 0, 0, 0};
+  if (wave >= 4)
+    block_l1_sp_role<true>(a, lds, lds_addr32(lds), wave, rows, nphase);
+  else
+    block_l1_sp_role<false>(a, lds, lds_addr32(lds), wave, rows, nphase);
+}
+
 int num_cus_b() {
   static int n = 0;
   if (!n) {
@@ -479,7 +743,11 @@ hipError_t launch_block_l1(const int8_t* x, int N, const int8_t* w1, const float
   if (f8)
     hipLaunchKernelGGL(block_l1_kernel<true>, dim3(N < grid ? N : grid), dim3(512), 0, s, a);
   else
+#ifdef DLQ_X_L1OLD
     hipLaunchKernelGGL(block_l1_kernel<false>, dim3(N < grid ? N : grid), dim3(512), 0, s, a);
+#else
+    hipLaunchKernelGGL(block_l1_sp_kernel, dim3(N < grid ? N : grid), dim3(512), 0, s, a);
+#endif
   return hipGetLastError();
 }
 

@@ -140,7 +140,9 @@ __device__ __forceinline__ void conv3x3i_init(const ConvArgs& a, int8_t* lds) {
 #endif
 }
 
-template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false>
+// RELU (int8, OUT == 0): the output clamp is [0, 127] and the requantisation
+// takes the v_cvt_pk_u8_f32 form (device_common.h quant4_relu).
+template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false, bool RELU = false>
 __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int mt, int f0, int lrank) {
   using G = IGeo<W>;
   constexpr int H = W, NS = C / ISC;
@@ -149,6 +151,15 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   static_assert(DPW <= 18, "at most two DMA pieces per tap");
   const bool loader = lrank >= 0;
   constexpr int STORES = OUT == 0 ? NF : 4 * NF;
+  // B fragments two taps ahead for the waves with <= 6 tiles: the younger
+  // wave of a SIMD pair runs alone at the end of every stage and, with its
+  // fragments only one tap (6 MFMAs) ahead, waited on LDS latency there;
+  // the 7-tile waves have no registers to spare for a second set
+#ifdef DLQ_X_PF1
+  constexpr bool PF2 = false;
+#else
+  constexpr bool PF2 = NF <= 6;
+#endif
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int lr = lane & 31, lh = lane >> 5;
@@ -352,6 +363,62 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
         }
       }
     } else {
+    if constexpr (PF2) {
+    // B fragments two taps ahead: fb[t & 1][f] holds tap t of tile f and is
+    // re-loaded with tap t + 2 right after the MFMA that consumed it (the
+    // LDS latency then has two taps of the SIMD's MFMAs to hide in, enough
+    // for a wave that runs alone at the end of a stage)
+    v4i fa[2], fb[2][NF];
+    auto ld_b = [&](int tap, int f) {
+      fb[tap & 1][f] = *(const v4i*)(lds + col_off[tap % 3][f] + (tap / 3) * G::RW * 16);
+    };
+    fa[0] = *(const v4i*)abase;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) ld_b(0, f);
+    fa[1] = *(const v4i*)(abase + 32);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) ld_b(1, f);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int bu = tap & 1;
+      const int k0 = tap * DPW / 9, k1 = (tap + 1) * DPW / 9;
+      if (dma) {
+#pragma unroll
+        for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
+      }
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        acc[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu], fb[bu][f], acc[f], 0, 0, 0);
+        if (f == NF - 1 && tap + 2 < 9) fa[bu] = *(const v4i*)(abase + (tap + 2) * 32);
+        if (tap + 2 < 9) ld_b(tap + 2, f);
+        if constexpr (OUT == 0 && RES) {
+          if (tap == 8 && j == NS - 1) {
+            const int p = cur_p0 + (f0 + f) * 32 + lr;
+            const bool keep = (f0 + f) * 32 + lr < IL && p < a.P;
+            const size_t off = keep ? (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16 : 0;
+            rq[f] = gload16_untracked(a.res + off);
+          }
+        }
+      }
+      if (tap + 2 < 9) {
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          if (i == NF - 1)
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read (B + the A two taps ahead)
+          else
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read (B)
+          if ((i == 1 && k1 > k0) || (i == 3 && k1 > k0 + 1))
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (LDS-DMA)
+        }
+      } else {
+        if (k1 > k0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        if (k1 > k0 + 1) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
+      }
+    }
+    } else {
     // A double-buffered per tap; each B fragment is re-loaded for the next
     // tap right after the MFMA that consumed it (one register set per tile).
     v4i fa[2], fb[NF];
@@ -405,6 +472,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
         __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
       }
     }
+    }  // PF2
     }  // int8 MFMA loop
 
     ISTAMP(2 + 2 * s);
@@ -463,6 +531,12 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
               q[g] = epi4_res_f8(ac, al[g], be[g], rg[g], a.s_res, lo);
             else
               q[g] = epi4_f8(ac, al[g], be[g], lo);
+          } else if constexpr (RELU) {
+            const int ac[4] = {acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
+            if constexpr (RES)
+              q[g] = epi4_res_relu(ac, al[g], be[g], rg[g], a.s_res);
+            else
+              q[g] = epi4_relu(ac, al[g], be[g]);
           } else {
             const int ac[4] = {acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
             if constexpr (RES)
@@ -486,7 +560,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   ISTAMP(63);
 }
 
-template <int W, int C, int OUT, bool RES, bool F8 = false>
+template <int W, int C, int OUT, bool RES, bool F8 = false, bool RELU = false>
 __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   using G = IGeo<W>;
   constexpr int OFF_AB = G::OFF_AB;
@@ -499,14 +573,14 @@ __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   wave_tiles<G::MT>(wave, mt, f0, nf);
   if constexpr (G::MT == 4) {
     if (nf == 7)
-      conv3x3i_body<W, C, OUT, RES, 7, 8, F8>(a, lds, mt, f0, wave);
+      conv3x3i_body<W, C, OUT, RES, 7, 8, F8, RELU>(a, lds, mt, f0, wave);
     else
-      conv3x3i_body<W, C, OUT, RES, 6, 8, F8>(a, lds, mt, f0, wave);
+      conv3x3i_body<W, C, OUT, RES, 6, 8, F8, RELU>(a, lds, mt, f0, wave);
   } else {
     if (nf == 4)
-      conv3x3i_body<W, C, OUT, RES, 4, 8, F8>(a, lds, mt, f0, wave);
+      conv3x3i_body<W, C, OUT, RES, 4, 8, F8, RELU>(a, lds, mt, f0, wave);
     else
-      conv3x3i_body<W, C, OUT, RES, 3, 8, F8>(a, lds, mt, f0, wave);
+      conv3x3i_body<W, C, OUT, RES, 3, 8, F8, RELU>(a, lds, mt, f0, wave);
   }
 }
 
@@ -528,6 +602,10 @@ hipError_t launch_ci(const ConvArgs& a, hipStream_t s) {
   const dim3 grid(NI < ncu ? NI : ncu), block(INW * 64);
   if (a.out_kind == 2)
     hipLaunchKernelGGL((conv3x3i_kernel<W, C, 2, false, F8>), grid, block, 0, s, a);
+  else if (!F8 && a.relu && a.res)
+    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, true, F8, true>), grid, block, 0, s, a);
+  else if (!F8 && a.relu)
+    hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, false, F8, true>), grid, block, 0, s, a);
   else if (a.res)
     hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, true, F8>), grid, block, 0, s, a);
   else

@@ -148,7 +148,10 @@ __device__ __forceinline__ int perm_at(int slot) {
     return g_perm7.px[slot];
 }
 
-template <int OW, int C, int OUT, bool DS, int NF, bool F8, bool RW>
+// RELU (int8, OUT == 0): conv1's clamp is [0, 127], requantised in the
+// v_cvt_pk_u8_f32 form (device_common.h quant4_relu); the downsample keeps
+// the signed clamp.
+template <int OW, int C, int OUT, bool DS, int NF, bool F8, bool RW, bool RELU = false>
 __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, const float* be_ds,
                                          int8_t* y_ds, int8_t* lds, int mt, int f0) {
   using G = JGeo<OW, DS, RW ? C / JSC : 0>;
@@ -467,7 +470,8 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
         }
       }
     } else {
-      auto epi = [&](const Acc* ac, int ab_off, float lo, int8_t* out) {
+      auto epi = [&](const Acc* ac, int ab_off, float lo, int8_t* out, auto rc) {
+        constexpr bool RL = decltype(rc)::value;
         float al[4][4], be[4][4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -488,6 +492,9 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
             if constexpr (F8) {
               const float a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
               q[g] = epi4_f8(a4, al[g], be[g], lo);
+            } else if constexpr (RL) {
+              const int a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
+              q[g] = epi4_relu(a4, al[g], be[g]);
             } else {
               const int a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
               q[g] = epi4(a4, al[g], be[g], lo);
@@ -503,8 +510,8 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
         }
       };
       constexpr float LO = F8 ? -448.f : -127.f;
-      epi(acc, 0, a.relu ? 0.f : LO, (int8_t*)a.y);
-      if constexpr (DS) epi(accd, 2 * OC * 4, LO, y_ds);
+      epi(acc, 0, a.relu ? 0.f : LO, (int8_t*)a.y, std::integral_constant<bool, RELU && !F8>{});
+      if constexpr (DS) epi(accd, 2 * OC * 4, LO, y_ds, std::integral_constant<bool, false>{});
     }
   }
   JSTAMP(62);
@@ -513,7 +520,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
 }
 
 // OUT: 0 = int8 (fused epilogues), 2 = int32 conv1 accumulators (DS = false).
-template <int OW, int C, int OUT, bool DS, bool F8, bool RW = false>
+template <int OW, int C, int OUT, bool DS, bool F8, bool RW = false, bool RELU = false>
 __global__ __launch_bounds__(JNW * 64, 1) void conv3x3s2i_kernel(ConvArgs a, const int8_t* w_ds, const float* al_ds,
                                                                  const float* be_ds, int8_t* y_ds) {
   using G = JGeo<OW, DS, RW ? C / JSC : 0>;
@@ -523,9 +530,9 @@ __global__ __launch_bounds__(JNW * 64, 1) void conv3x3s2i_kernel(ConvArgs a, con
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
   const int wave = threadIdx.x >> 6;
   if (wave < 4)
-    s2i_body<OW, C, OUT, DS, 4, F8, RW>(a, w_ds, al_ds, be_ds, y_ds, lds, wave & 3, 0);
+    s2i_body<OW, C, OUT, DS, 4, F8, RW, RELU>(a, w_ds, al_ds, be_ds, y_ds, lds, wave & 3, 0);
   else
-    s2i_body<OW, C, OUT, DS, 3, F8, RW>(a, w_ds, al_ds, be_ds, y_ds, lds, wave & 3, 4);
+    s2i_body<OW, C, OUT, DS, 3, F8, RW, RELU>(a, w_ds, al_ds, be_ds, y_ds, lds, wave & 3, 4);
 }
 
 int num_cus_s2i() {
@@ -549,14 +556,23 @@ hipError_t launch_j(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, c
     hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 2, false, F8>), grid, block, 0, s, a, nullptr, nullptr, nullptr,
                        nullptr);
   } else if (w_ds) {
+    const bool relu = !F8 && a.relu;  // conv1's clamp [0, 127]: the v_cvt_pk_u8_f32 epilogue
     if constexpr (OW == 28 && C == 64) {  // layer2.0: one output-channel tile -> resident weights
       if (a.OCp == JOT) {
-        hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true, F8, true>), grid, block, 0, s, a, w_ds, al_ds, be_ds,
-                           y_ds);
+        if (relu)
+          hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true, F8, true, true>), grid, block, 0, s, a, w_ds, al_ds,
+                             be_ds, y_ds);
+        else
+          hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true, F8, true>), grid, block, 0, s, a, w_ds, al_ds, be_ds,
+                             y_ds);
         return hipGetLastError();
       }
     }
-    hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true, F8>), grid, block, 0, s, a, w_ds, al_ds, be_ds, y_ds);
+    if (relu)
+      hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true, F8, false, true>), grid, block, 0, s, a, w_ds, al_ds,
+                         be_ds, y_ds);
+    else
+      hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true, F8>), grid, block, 0, s, a, w_ds, al_ds, be_ds, y_ds);
   } else {
     hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, false, F8>), grid, block, 0, s, a, nullptr, nullptr, nullptr,
                        nullptr);

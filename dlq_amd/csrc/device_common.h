@@ -73,6 +73,32 @@ __device__ __forceinline__ unsigned epi4_res(const int* acc, const float* al, co
          __builtin_amdgcn_perm(__float_as_uint(c23[1]), __float_as_uint(c23[0]), 0x04000c0cu);
 }
 
+// ReLU requantisation without the med3 / magic-number / perm sequence:
+// rne(clamp(y, 0, 127)) = v_cvt_pk_u8_f32(min(y, 127)), which rounds to
+// nearest even, saturates at 0 and inserts the byte in one instruction
+// (equal on every fp32 pattern of [-2, 300] and a stride of the whole finite
+// range: tools/probe/cvt_pk_u8_probe.hip).  Byte e = value e, as quant4.
+__device__ __forceinline__ unsigned quant4_relu(float y0, float y1, float y2, float y3) {
+  unsigned r = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(y0, 127.f), 0, 0u);
+  r = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(y1, 127.f), 1, r);
+  r = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(y2, 127.f), 2, r);
+  return __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(y3, 127.f), 3, r);
+}
+__device__ __forceinline__ unsigned epi4_relu(const int* acc, const float* al, const float* be) {
+  const v2f y01 = __builtin_elementwise_fma(v2f{(float)acc[0], (float)acc[1]}, v2f{al[0], al[1]}, v2f{be[0], be[1]});
+  const v2f y23 = __builtin_elementwise_fma(v2f{(float)acc[2], (float)acc[3]}, v2f{al[2], al[3]}, v2f{be[2], be[3]});
+  return quant4_relu(y01[0], y01[1], y23[0], y23[1]);
+}
+__device__ __forceinline__ unsigned epi4_res_relu(const int* acc, const float* al, const float* be, unsigned r4,
+                                                  float r_s) {
+  const v2f s = {r_s, r_s};
+  v2f y01 = __builtin_elementwise_fma(v2f{(float)acc[0], (float)acc[1]}, v2f{al[0], al[1]}, v2f{be[0], be[1]});
+  v2f y23 = __builtin_elementwise_fma(v2f{(float)acc[2], (float)acc[3]}, v2f{al[2], al[3]}, v2f{be[2], be[3]});
+  y01 = __builtin_elementwise_fma(v2f{(float)(int)(signed char)r4, (float)(int)(signed char)(r4 >> 8)}, s, y01);
+  y23 = __builtin_elementwise_fma(v2f{(float)(int)(signed char)(r4 >> 16), (float)((int)r4 >> 24)}, s, y23);
+  return quant4_relu(y01[0], y01[1], y23[0], y23[1]);
+}
+
 // ---- fp8 (e4m3, OCP) helpers: DESIGN.md §3b, oracle.c ora_*_f8 ----------
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef int v8i __attribute__((ext_vector_type(8)));
