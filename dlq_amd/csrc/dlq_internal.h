@@ -37,6 +37,10 @@ struct ConvArgs {
 #endif
 
 // Stem packing: C == 4, 7x7 taps padded to 8x8 -> K = 256.
+// Largest batch an engine may prepare: the conv kernels compute activation
+// offsets as int ((n*H + h)*W + w)*C (layer1's 200,704 B per image at
+// 8192 images is 1.64e9 < 2^31; tools/check/dma_plan.py proves the bound).
+constexpr int kMaxBatch = 8192;
 constexpr int kStemC = 4;
 constexpr int kStemK = 8 * 8 * 4;
 
@@ -82,6 +86,10 @@ hipError_t launch_gap(const int8_t* x, int N, int C, int HW, float k, int8_t* y,
 hipError_t launch_gap4(const int8_t* x, int N, int C, int HW, float k, int8_t* y, hipStream_t s);  // C % 4 == 0
 hipError_t launch_linear(const int8_t* x, int N, int K, const int8_t* w, int OC, const float* alpha,
                          const float* beta, int relu, int out_kind, void* y, hipStream_t s);
+// One-launch int8 MLP (quantise -> fc1 + bias + ReLU + requant -> fc2 + bias), head.hip.
+hipError_t launch_mlp_fused(const float* x, int N, int in, int kp, float inv_s, const int8_t* w1, int H,
+                            const float* a1, const float* b1, const int8_t* w2, int OC, const float* a2,
+                            const float* b2, int8_t* hq, float* y, hipStream_t s, int mr = 0);
 hipError_t launch_gap_fc(const int8_t* x, int N, int C, int HW, float k, const int8_t* w, int OC,
                          const float* alpha, const float* beta, float* y, hipStream_t s);  // C == 512, HW <= 56
 // dlq_gemm_s8s8s32 (gemm.hip): row-major int8 A[M][K] . B[K][N] -> int32 C.

@@ -228,7 +228,238 @@ __global__ __launch_bounds__(256) void gap_fc_kernel(const int8_t* __restrict__ 
   }
 }
 
+// One-launch int8 MLP forward (the MNIST forward of CUDA/MNIST_on_GPU/v4.cu:
+// 255-302 -- matmul_a_b + bias_forward + relu_forward, matmul_a_b +
+// bias_forward -- and v5.cu:127-157).  The forward is 0.2 GOP: what bounds it
+// is instructions and memory round trips per wave, so the grid spreads it over
+// every CU (MLP_MR = 4 rows per workgroup: 256 workgroups at B = 1024, one
+// wave per SIMD) and each wave waits for memory about once:
+//   0. each wave issues its input-row loads, one epilogue constant of each
+//      kind per thread, and the weight fragments of its first fc1 tile (all 26 k-steps of MNIST's
+//      K = 832) and of its fc2 tile;
+//   1. the rows -> q = clamp(rne(x * inv_s)) into LDS (quantize_rows_kernel's
+//      op sequence; zeros beyond `in`);
+//   2. fc1 on v_mfma_i32_32x32x32_i8 (A = 32 hidden units of the packed
+//      weights, B = the LDS rows, lane l reading row l & 3), epilogue
+//      fmaf(acc, a1, b1), ReLU, requant into LDS (and the global hidden buffer
+//      dlq_mlp_copy_hidden reads);
+//   3. fc2 from LDS, epilogue fmaf(acc, a2, b2) -> fp32 logits.
+// Per element the same integer sums and IEEE ops as quantize_rows_kernel +
+// linear_kernel<0> + linear_kernel<1>: bit-identical to the three-launch
+// forward.  Every load reads a valid (clamped) address outside any branch (a
+// load on one side of a branch costs a vmcnt(0) at the join); values past the
+// ends are never used.
+#ifdef DLQ_STAMPS
+__device__ unsigned long long g_mlp_stamps[1024 * 4 * 8];
+#define MSTAMP(i)                                                                                            \
+  do {                                                                                                       \
+    if ((threadIdx.x & 63) == 0) g_mlp_stamps[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define MSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+constexpr int MLP_NW = 4;   // waves
+constexpr int MLP_MR_DEFAULT = 4;
+constexpr int MLP_KB = 26;  // fc1 k-steps per register batch (K = 832)
+constexpr int MLP_W2 = 8;   // fc2 k-steps prefetched at kernel start (H <= 256)
+
+__device__ __forceinline__ v4i mlp_wfrag(const int8_t* wp, size_t ws, int k, int lh, int sw) {
+  const int lc = (2 * k + lh) & 3;  // generic packed image: chunk (2k + lh) & 3 of 64-deep block k >> 1
+  return *(const v4i*)(wp + (size_t)(k >> 1) * ws + ((lc ^ sw) << 4));
+}
+// n k-steps of fragments from k-step kb on: a wave-uniform block pointer
+// bumped once per 64-deep block (never past the last block) + per-lane 32-bit
+// offsets for even / odd k (row + XOR'd chunk), i.e. a scalar add and a
+// global_load in the saddr form per fragment.  kb and nk are even.
+template <int NF>
+__device__ __forceinline__ void mlp_wfrags(const int8_t* w, size_t ws, int kb, int nk, const unsigned (&offs)[2],
+                                           v4i (&f)[NF]) {
+  const int8_t* wk = w + (size_t)(kb >> 1) * ws;
+#pragma unroll
+  for (int i = 0; i < NF; i += 2) {
+    f[i] = *(const v4i*)(wk + offs[0]);
+    if (i + 1 < NF) f[i + 1] = *(const v4i*)(wk + offs[1]);
+    wk += kb + i + 2 < nk ? ws : 0;
+  }
+}
+
+template <int MLP_MR>  // rows per workgroup (= input float4 loads per thread issued up front)
+__global__ __launch_bounds__(MLP_NW * 64) void mlp_fused_kernel(
+    const float* __restrict__ x, int N, int in, int kp, float inv_s, const int8_t* __restrict__ w1, int H,
+    int OCp1, const float* __restrict__ a1, const float* __restrict__ b1, const int8_t* __restrict__ w2, int OC,
+    int OCp2, const float* __restrict__ a2, const float* __restrict__ b2, int8_t* __restrict__ hq_g,
+    float* __restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) int8_t mlp_lds[];
+  const int xp = kp + 16, hp = H + 16;
+  int8_t* xq = mlp_lds;
+  int8_t* hq = xq + MLP_MR * xp;
+  float* ab = (float*)(hq + MLP_MR * hp);  // a1[H] b1[H] a2[OCp2] b2[OCp2]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 31, lh = lane >> 5;
+  const int r0 = blockIdx.x * MLP_MR, br = lr & (MLP_MR - 1), nrow = min(MLP_MR, N - r0);
+  const int T = H / 32, T2 = (OC + 31) / 32, nk1 = kp / 32, nk2 = H / 32, u4 = kp >> 2;
+  const size_t ws1 = (size_t)(OCp1 / 64) * 64 * 64, ws2 = (size_t)(OCp2 / 64) * 64 * 64;
+  MSTAMP(0);
+
+  // 0. loads, in the order of need (vmcnt counts in issue order)
+  const bool vec = (in & 3) == 0 && u4 <= MLP_NW * 64;  // one float4 per thread and row (MNIST: 196 per row)
+  float4 f[MLP_MR];
+  if (vec) {
+    const unsigned xo = (unsigned)min(4 * tid, in - 4) * 4u;
+#pragma unroll
+    for (int r = 0; r < MLP_MR; ++r)
+      f[r] = *(const float4*)((const char*)(x + (size_t)(r0 + min(r, nrow - 1)) * in) + xo);
+  }
+  const int oc1 = min(wave, T - 1) * 32 + lr, ol1 = oc1 & 63, sw1 = (ol1 >> 2) & 3;
+  const int oc2 = min(wave, T2 - 1) * 32 + lr, ol2 = oc2 & 63, sw2 = (ol2 >> 2) & 3;
+  const int8_t* wp1 = w1 + ((size_t)(oc1 >> 6) * 64 + ol1) * 64;
+  const int8_t* wp2 = w2 + ((size_t)(oc2 >> 6) * 64 + ol2) * 64;
+  // epilogue constants, one of each per thread (to LDS after the quantisation)
+  const float ca1 = a1[min(tid, H - 1)], cb1 = b1[min(tid, H - 1)];
+  const float ca2 = a2[min(tid, OC - 1)], cb2 = b2[min(tid, OC - 1)];
+  const unsigned o1[2] = {(unsigned)(wp1 - w1) + (unsigned)(((0 + lh) ^ sw1) << 4),
+                          (unsigned)(wp1 - w1) + (unsigned)(((2 + lh) ^ sw1) << 4)};
+  const unsigned o2[2] = {(unsigned)(wp2 - w2) + (unsigned)(((0 + lh) ^ sw2) << 4),
+                          (unsigned)(wp2 - w2) + (unsigned)(((2 + lh) ^ sw2) << 4)};
+  v4i fa[MLP_KB];
+  mlp_wfrags(w1, ws1, 0, nk1, o1, fa);
+  v4i f2[MLP_W2];
+  mlp_wfrags(w2, ws2, 0, nk2, o2, f2);
+  MSTAMP(1);
+
+  // 1. quantise the rows into LDS
+  auto quant = [&](float v0, float v1, float v2, float v3) -> unsigned {
+    return ((unsigned)sat_rne(v0 * inv_s) & 0xffu) | (((unsigned)sat_rne(v1 * inv_s) & 0xffu) << 8) |
+           (((unsigned)sat_rne(v2 * inv_s) & 0xffu) << 16) | (((unsigned)sat_rne(v3 * inv_s) & 0xffu) << 24);
+  };
+  if (vec) {
+#pragma unroll
+    for (int r = 0; r < MLP_MR; ++r) {
+      const bool ok = r < nrow && 4 * tid < in;
+      if (tid < u4)
+        *(unsigned*)(xq + r * xp + 4 * tid) =
+            quant(ok ? f[r].x : 0.f, ok ? f[r].y : 0.f, ok ? f[r].z : 0.f, ok ? f[r].w : 0.f);
+    }
+  } else {
+    for (int u = tid; u < MLP_MR * u4; u += MLP_NW * 64) {
+      const int r = u / u4, c0 = 4 * (u - r * u4), row = r0 + r;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = row < N && c0 + e < in ? x[(size_t)row * in + c0 + e] : 0.f;
+      *(unsigned*)(xq + r * xp + c0) = quant(v[0], v[1], v[2], v[3]);
+    }
+  }
+  if (tid < H) {
+    ab[tid] = ca1;
+    ab[H + tid] = cb1;
+  }
+  if (tid < OC) {
+    ab[2 * H + tid] = ca2;
+    ab[2 * H + OCp2 + tid] = cb2;
+  }
+  for (int i = MLP_NW * 64 + tid; i < H; i += MLP_NW * 64) {
+    ab[i] = a1[i];
+    ab[H + i] = b1[i];
+  }
+  for (int i = MLP_NW * 64 + tid; i < OC; i += MLP_NW * 64) {
+    ab[2 * H + i] = a2[i];
+    ab[2 * H + OCp2 + i] = b2[i];
+  }
+  __syncthreads();
+  MSTAMP(2);
+
+  // 2. fc1 + bias + ReLU + requant: tiles wave, wave + 4, ...
+  for (int ot = wave; ot < T; ot += MLP_NW) {
+    const int oc = ot * 32 + lr, ol = oc & 63, sw = (ol >> 2) & 3;
+    const unsigned ro = (unsigned)(((oc >> 6) * 64 + ol) * 64);
+    const unsigned ot_o[2] = {ro + (unsigned)(((0 + lh) ^ sw) << 4), ro + (unsigned)(((2 + lh) ^ sw) << 4)};
+    v16i acc = v16i{0}, acc1 = v16i{0};  // even / odd k-steps: two MFMA chains, summed (exact int32)
+    for (int kb = 0; kb < nk1; kb += MLP_KB) {
+      if (kb > 0 || ot != wave) mlp_wfrags(w1, ws1, kb, nk1, ot_o, fa);
+#pragma unroll
+      for (int i = 0; i < MLP_KB; ++i)
+        if (kb + i < nk1) {  // wave-uniform
+          const v4i bf = *(const v4i*)(xq + br * xp + (kb + i) * 32 + lh * 16);
+          if (i & 1)
+            acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], bf, acc1, 0, 0, 0);
+          else
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], bf, acc, 0, 0, 0);
+        }
+    }
+    acc += acc1;
+    if (lr < MLP_MR) {  // D column lr = row r0 + lr
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int o0 = ot * 32 + 8 * g + 4 * lh;
+        const v4i al = *(const v4i*)(ab + o0), be = *(const v4i*)(ab + H + o0);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf((float)acc[4 * g + e], __int_as_float(al[e]), __int_as_float(be[e]));
+        const unsigned q = quant4(v[0], v[1], v[2], v[3], 0.f);
+        *(unsigned*)(hq + lr * hp + o0) = q;
+        if (lr < nrow) *(unsigned*)(hq_g + (size_t)(r0 + lr) * H + o0) = q;
+      }
+    }
+  }
+  __syncthreads();
+  MSTAMP(3);
+
+  // 3. fc2 + bias -> fp32 logits
+  for (int ot = wave; ot < T2; ot += MLP_NW) {
+    const int oc = ot * 32 + lr, ol = oc & 63, sw = (ol >> 2) & 3;
+    const int8_t* wp = w2 + ((size_t)(oc >> 6) * 64 + ol) * 64;
+    v16i acc = v16i{0};
+#pragma unroll
+    for (int k = 0; k < MLP_W2; ++k)
+      if (k < nk2) {
+        const v4i a = ot == wave ? f2[k] : mlp_wfrag(wp, ws2, k, lh, sw);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, *(const v4i*)(hq + br * hp + k * 32 + lh * 16), acc, 0, 0, 0);
+      }
+    for (int k = MLP_W2; k < nk2; ++k)
+      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(mlp_wfrag(wp, ws2, k, lh, sw),
+                                                  *(const v4i*)(hq + br * hp + k * 32 + lh * 16), acc, 0, 0, 0);
+    if (lr < nrow) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int o0 = ot * 32 + 8 * g + 4 * lh;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (o0 + e < OC)
+            y[(size_t)(r0 + lr) * OC + o0 + e] =
+                __builtin_fmaf((float)acc[4 * g + e], ab[2 * H + o0 + e], ab[2 * H + OCp2 + o0 + e]);
+      }
+    }
+  }
+  MSTAMP(4);
+}
+
 }  // namespace
+
+// The fused MNIST forward: kp % 64 == 0, kp >= in, H % 64 == 0.
+template <int MR>
+hipError_t launch_mlp_mr(const float* x, int N, int in, int kp, float inv_s, const int8_t* w1, int H,
+                         const float* a1, const float* b1, const int8_t* w2, int OC, const float* a2,
+                         const float* b2, int8_t* hq, float* y, hipStream_t s) {
+  const size_t lds = (size_t)MR * (kp + 16) + (size_t)MR * (H + 16) + (size_t)(2 * H + 2 * packed_oc(OC)) * 4;
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mlp_fused_kernel<MR>, dim3((N + MR - 1) / MR), dim3(MLP_NW * 64), lds, s, x, N, in, kp, inv_s,
+                     w1, H, packed_oc(H), a1, b1, w2, OC, packed_oc(OC), a2, b2, hq, y);
+  return hipGetLastError();
+}
+
+// The fused MNIST forward: kp % 64 == 0, kp >= in, H % 64 == 0.  mr = rows
+// per workgroup (4, 8 or 16; 0 = the default for N).
+hipError_t launch_mlp_fused(const float* x, int N, int in, int kp, float inv_s, const int8_t* w1, int H,
+                            const float* a1, const float* b1, const int8_t* w2, int OC, const float* a2,
+                            const float* b2, int8_t* hq, float* y, hipStream_t s, int mr) {
+  if (N < 1 || in < 1 || kp % 64 || kp < in || H < 64 || H % 64 || OC < 1) return hipErrorInvalidValue;
+  if (mr == 0) mr = MLP_MR_DEFAULT;
+  if (mr == 4) return launch_mlp_mr<4>(x, N, in, kp, inv_s, w1, H, a1, b1, w2, OC, a2, b2, hq, y, s);
+  if (mr == 8) return launch_mlp_mr<8>(x, N, in, kp, inv_s, w1, H, a1, b1, w2, OC, a2, b2, hq, y, s);
+  if (mr == 16) return launch_mlp_mr<16>(x, N, in, kp, inv_s, w1, H, a1, b1, w2, OC, a2, b2, hq, y, s);
+  return hipErrorInvalidValue;
+}
 
 // C = K = 512, HW <= 56 (the ResNet-18 head); hipErrorInvalidValue otherwise.
 hipError_t launch_gap_fc(const int8_t* x, int N, int C, int HW, float k, const int8_t* w, int OC,

@@ -5,9 +5,10 @@
 // -> matmul_a_b_kernel -> bias_forward_kernel) and v5.cu forward_pass_only
 // (:127-157, cublasSgemm + bias_add_kernel + relu_kernel).  The softmax
 // (v4.cu:182-200) and the training half (backward, SGD) are out of scope.
-// Each layer is ONE launch of the int8 MFMA GEMM with bias, ReLU and the
-// requantisation fused into its epilogue; the reference issues three kernels
-// and a cudaDeviceSynchronize per op (v4.cu:260-265).
+// The whole forward is ONE launch (head.hip mlp_fused_kernel: quantise, fc1 +
+// bias + ReLU + requant, fc2 + bias, the hidden layer kept in LDS); the
+// reference issues five kernels and a cudaDeviceSynchronize per op
+// (v4.cu:260-265).
 #include <cstring>
 #include <vector>
 
@@ -107,11 +108,9 @@ int dlq_mlp_forward(dlq_mlp* m, const float* x, int B, float* logits, void* stre
   if (B < 0 || B > m->max_batch) return fail(DLQ_ERR_ARG, "mlp_forward: batch exceeds max_batch");
   if (B == 0) return DLQ_OK;
   if (!x || !logits) return fail(DLQ_ERR_ARG, "mlp_forward: null argument");
-  int rc = dlq_quantize_rows_s8(x, B, m->in, m->kp, 1.0f / m->s_in, m->xq, stream);
-  if (rc) return rc;
-  rc = dlq_linear_s8(m->xq, B, m->kp, m->w1, m->hidden, m->a1, m->b1, 1, DLQ_OUT_S8, m->hq, stream);
-  if (rc) return rc;
-  return dlq_linear_s8(m->hq, B, m->hidden, m->w2, m->out, m->a2, m->b2, 0, DLQ_OUT_F32, logits, stream);
+  const hipError_t e = launch_mlp_fused(x, B, m->in, m->kp, 1.0f / m->s_in, m->w1, m->hidden, m->a1, m->b1, m->w2,
+                                        m->out, m->a2, m->b2, m->hq, logits, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : hip_fail(e, "mlp_forward");
 }
 
 int dlq_mlp_copy_hidden(const dlq_mlp* m, int B, int8_t* dst, size_t cap, void* stream) {

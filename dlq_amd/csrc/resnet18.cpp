@@ -706,6 +706,7 @@ int dlq_resnet18_set_precision(dlq_resnet18* m, int precision) {
 
 int dlq_resnet18_prepare(dlq_resnet18* m, int max_batch, void* stream) {
   if (!m || max_batch <= 0) return fail(DLQ_ERR_ARG, "prepare: bad args");
+  if (max_batch > kMaxBatch) return fail(DLQ_ERR_ARG, "prepare: max_batch above kMaxBatch (int32 activation offsets)");
   int rc = check_ready(m);
   if (rc) return rc;
   free_all(m);

@@ -412,3 +412,35 @@ def test_mnist_mlp_bitexact(gpu, hidden):
     for B in (1, 3, 77):
         o2 = m(_cuda(x[:B])).cpu().numpy()
         assert np.array_equal(o2.view(np.int32), ref[:B].view(np.int32))
+
+
+@pytest.mark.parametrize("inp,hidden,out,B", [(100, 64, 10, 50), (784, 192, 10, 1000), (257, 512, 37, 33),
+                                              (784, 1024, 10, 64), (130, 128, 3, 17)])
+def test_mlp_fused_shapes_bitexact(gpu, inp, hidden, out, B):
+    """The one-launch MLP (head.hip mlp_fused_kernel) off the MNIST shape: `in`
+    not a multiple of 4 or 64 (scalar loads, zero K tail), K split over waves
+    (hidden < 256) or several tiles per wave (hidden > 256), more than one fc2
+    tile, ragged row blocks -- int32 sums and epilogues bit-exact vs the oracle."""
+    from dlq_amd.models import MLPInt8, mlp_weights
+    from dlq_amd.quant import calibrate_mlp
+    W1, b1, W2, b2 = mlp_weights(inp, hidden, out, seed=inp + hidden)
+    b1 = (np.random.default_rng(3).standard_normal(hidden) * 0.1).astype(np.float32)
+    b2 = (np.random.default_rng(4).standard_normal(out) * 0.1).astype(np.float32)
+    rng = np.random.default_rng(inp * 7 + B)
+    x = (rng.standard_normal((B, inp)) * 1.5).astype(np.float32)
+    s_in, s_h = calibrate_mlp(W1, b1, x)
+    xq = O.quantize_f32_s8(x, s_in)
+    q1, sw1 = O.quantize_weights_s8(W1.T.copy())
+    q2, sw2 = O.quantize_weights_s8(W2.T.copy())
+    acc1 = np.empty((B, hidden), np.int32)
+    O.lib().ora_mlp_layer_s8_acc(xq, q1.T.copy(), B, inp, hidden, acc1)
+    a1, bb1 = O.mlp_alpha_beta(s_in, sw1, b1, s_h)
+    h = O.epilogue_s8(acc1[:, :, None], a1, bb1, relu=True)[:, :, 0]
+    acc2 = np.empty((B, out), np.int32)
+    O.lib().ora_mlp_layer_s8_acc(h, q2.T.copy(), B, hidden, out, acc2)
+    ref = np.empty((B, out), np.float32)
+    O.lib().ora_epilogue_f32(acc2.reshape(-1), B, out, 1, O.fc_alpha(s_h, sw2), b2, 0, ref)
+    m = MLPInt8(W1, b1, W2, b2, s_in, s_h, max_batch=B)
+    got = m(_cuda(x)).cpu().numpy()
+    assert np.array_equal(m.hidden_q(B).cpu().numpy(), h)
+    assert np.array_equal(got.view(np.int32), ref.view(np.int32))
