@@ -7,30 +7,43 @@
 // and maxpool2d_3x3_s2p1_nchw (:282-293).  The 112x112x64 conv1 output never
 // leaves the register file.
 //
-// Input: every thread loads the fp32 values of its half super-pixel straight
-// into registers (three 8-byte loads, one per channel: 64 lanes read 512
-// contiguous bytes of an input row), PD steps ahead of their use, and
-// quantises them into a ring of "super rows": 2x2 pixels x (RGB, 0) = 16-byte
-// super-pixels, so the
-// 7x7/s2 conv is a 4x4/s1 conv over super-pixels (kh = 2*ky+dy-1; kh = -1
-// carries a zero weight) with K = 16 super taps x 16 B = 8 steps of
-// v_mfma_i32_32x32x32_i8, every A fragment one ds_read_b128.
+// K packing ("column units"): conv1's 147 taps per output pixel are 12 units
+// of 16 bytes, unit (c, j) = channel c, input columns 2(ox-2+j) + {0, 1}
+// (dx), the conv row's 8 input rows 2oy-3 .. 2oy+4 (kh): byte 2 kh + dx.
+// K = 3 c x 4 j x 16 = 192 = 6 steps of v_mfma_i32_32x32x32_i8 (kw = 2j+dx-1
+// = -1 and kh = 7 carry zero weights; the previous 2x2 space-to-depth packing
+// padded 147 to 256).  Consecutive conv columns are consecutive units, so an
+// A fragment is ONE aligned ds_read_b128 (2-byte-aligned 8-byte reads of a
+// row-major plane cost 7x the LDS cycles: tools/probe/lds_tput_probe.hip).
+// The units live in a ring of 8 conv-row buffers; the converter scatters
+// each quantised input pixel pair (2 bytes, one ds_write_b16) into the 4
+// conv rows whose window holds its input row.
 //
-// MFMA orientation D[px][oc]: A = 32 conv pixels of one conv row, B = 32 output
-// channels held in registers for the whole kernel.  A-row i is conv column
-// c0 + pi(i) with pi chosen so that D register r of lane half h holds column
-// c0 + 16h + r: each lane owns 16 consecutive columns of ONE channel, and the
-// 3x3/s2 max pool runs on the int32 accumulators in registers (v_max3_i32).
-// Pooling before the epilogue is exact because the epilogue y = fma(acc, a, b)
-// -> clamp -> rne is monotone non-decreasing in acc once a >= 0; channels with
-// a < 0 have their weights (and a) negated at packing time
-// (dlq_pack_stem_weights_s8).  Only the pooled values (1/4 of the conv
-// outputs) are requantised.
+// Input: every thread loads 2 pixels x 3 channels of one input row of one
+// column unit (three 8-byte loads; a wave's 64 lanes are 16 units x 4 rows, so
+// its ds_write_b16 scatter touches each bank at most twice) straight into
+// registers, PD = 4 row quads ahead of their conversion.
 //
-// Work item = (image, band of pooled rows).  8 waves = 2 channel tiles x 4
-// column quarters; quarter q computes conv columns 28q-1 .. 28q+30 (32, of
-// which 29 are used) and produces pooled columns 14q .. 14q+13.  A step
-// computes conv rows 2p, 2p+1 and emits pooled row p.
+// MFMA orientation D[px][oc]: A = 32 conv pixels of one conv row, B = the
+// wave's 32 output channels (weight image in LDS, 208-byte rows).  A-row i is
+// conv column c0 + pi(i) with pi chosen so that D register r of lane half h
+// holds column c0 + 16h + r: each lane owns 16 consecutive columns of ONE
+// channel, and the 3x3/s2 max pool runs on the int32 accumulators in
+// registers (v_max3_i32).  Pooling before the epilogue is exact because the
+// epilogue y = fma(acc, a, b) -> clamp -> rne is monotone non-decreasing in
+// acc once a >= 0; channels with a < 0 have their weights (and a) negated at
+// packing time (dlq_pack_stem_weights_s8).  Only the pooled values (1/4 of
+// the conv outputs) are requantised.
+//
+// Work item = (image, band of pooled rows); workgroup = 8 waves = 4 column
+// quarters x 2 channel tiles, two workgroups per CU.  Quarter q computes conv
+// columns 28q-1 .. 28q+30 (32, of which 29 are used) and produces pooled
+// columns 14q .. 14q+13.  A step computes conv rows 2p, 2p+1 and emits pooled
+// row p.  Measured (tools/probe/stem_stamps.hip, N = 256, same box): 77.5 ->
+// 72.5 us against the space-to-depth kernel; the launch runs at ~1.3 GHz
+// (s_memtime cycles / wall), i.e. at the chip's power limit, not at HBM (the
+// same input access pattern alone streams at 6.0 TB/s:
+// tools/probe/stem_stream_probe.hip).
 #include <cmath>
 #include <type_traits>
 #include <utility>
@@ -40,16 +53,19 @@
 namespace dlq {
 namespace {
 
-constexpr int SNW = 8;                   // waves
-constexpr int PD = 2;                    // super-row pairs whose input loads are in flight ahead of the converter
-constexpr int PATCH_SLOTS = 8;           // super-row ring
-constexpr int PATCH_ROW = 128 * 16;      // super cols -4 .. 123
-constexpr int OFF_PATCH = 0;
-constexpr int OFF_STAGE = OFF_PATCH + PATCH_SLOTS * PATCH_ROW;  // per wave 16 x 32 B output staging
-constexpr int WPITCH_S = 256 + 16;       // weight row pitch (17 units: a lane group's 16 rows on 16 bank quads)
-constexpr int OFF_WST = OFF_STAGE + SNW * 512;                  // the 64 x 256 B weight image
-constexpr int LDS_STEM = OFF_WST + 64 * WPITCH_S;               // 37 KiB: two workgroups per CU
-static_assert(LDS_STEM <= 160 * 1024, "LDS budget");
+constexpr int SNW = 8;                   // waves: 4 column quarters x 2 channel tiles
+constexpr int PD = 4;                    // row quads whose input loads are in flight ahead of the converter
+constexpr int CR_SLOTS = 8;              // conv-row ring
+constexpr int CR_PLANE = 128 * 16;       // one channel: units = super cols -4 .. 123 (0..3, 116..127 zero)
+constexpr int CR_ROW = 3 * CR_PLANE + 64;  // conv-row slot pitch (+16 banks: adjacent slots' scatters on other banks)
+constexpr int OFF_CR = 0;
+constexpr int STG = 16 * 32;             // per wave: 16 pooled pixels x 32 channels of output staging
+constexpr int OFF_STAGE = OFF_CR + CR_SLOTS * CR_ROW;
+constexpr int WPITCH_S = 192 + 16;      // weight row pitch (13 units: a lane group's 16 rows on 16 bank quads)
+constexpr int OFF_WST = OFF_STAGE + SNW * STG;  // the 64 x 192 B weight image
+constexpr int LDS_STEM = OFF_WST + 64 * WPITCH_S;  // 66 KiB: two workgroups per CU
+static_assert(2 * LDS_STEM <= 160 * 1024, "two workgroups per CU");
+constexpr int SK = 192;                  // packed K per output channel
 constexpr int kIntMin = (int)0x80000000;
 
 #ifdef DLQ_STAMPS
@@ -79,7 +95,7 @@ __device__ unsigned long long g_sstamps[512 * 8 * 8];
 
 struct StemArgs {
   const float* x;      // [N][3][224][224]
-  const int8_t* w;     // [64][16 super taps][16 B] (dlq_pack_stem_weights_s8)
+  const int8_t* w;     // [64 oc][6 k-steps][2 lane halves][16 B] (dlq_pack_stem_weights_s8)
   const float* alpha;  // [64] |alpha| (packed), output-grid units
   const float* beta;   // [64]
   int8_t* y;           // [N][56][56][64]
@@ -92,12 +108,11 @@ __device__ __forceinline__ int max3i(int a, int b, int c) {
   return __builtin_elementwise_max(__builtin_elementwise_max(a, b), c);
 }
 
-// F8: the fp8 path: the input is quantised to e4m3 (enc4_f8),
-// the 8 i8 k-steps become 4 v_mfma_f32_32x32x64_f8f6f4 (k-steps 2i, 2i+1 as
-// the two halves of each 32-byte fragment, A and B alike), the pool runs on
-// the fp32 accumulators (max is exact; the e4m3 epilogue is monotone once
-// alpha >= 0: dlq_pack_stem_weights_f8 flips the sign bits of the rows with
-// alpha < 0).
+// F8: the fp8 path: the input is quantised to e4m3, the 6 i8
+// k-steps become 3 v_mfma_f32_32x32x64_f8f6f4 (k-steps 2i, 2i+1 as the two
+// halves of each 32-byte fragment, A and B alike), the pool runs on the fp32
+// accumulators (max is exact; the e4m3 epilogue is monotone once alpha >= 0:
+// dlq_pack_stem_weights_f8 flips the sign bits of the rows with alpha < 0).
 template <bool F8>
 __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
   using Acc = typename std::conditional<F8, v16f, v16i>::type;
@@ -109,39 +124,44 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
   const int ot = wave & 1, q = wave >> 1;  // channel tile, column quarter
   const int nitems = a.N * a.nb;
 
-  // The weight image in LDS (B fragments re-read per conv row: registers go to
-  // the second co-resident workgroup), and the channel's epilogue constants.
-  for (int i = tid; i < 64 * 16; i += SNW * 64)
-    *(v4i*)(lds + OFF_WST + (i >> 4) * WPITCH_S + (i & 15) * 16) = *(const v4i*)(a.w + i * 16);
-  const int8_t* wlds = lds + OFF_WST + (ot * 32 + lr) * WPITCH_S + lh * 16;
+  // The weight image in LDS (B fragments re-read per conv row: the
+  // registers hold the input loads in flight) and the channel's epilogue
+  // constants.
+  for (int i = tid; i < 64 * 12; i += SNW * 64)
+    *(v4i*)(lds + OFF_WST + (i / 12) * WPITCH_S + (i % 12) * 16) = *(const v4i*)(a.w + i * 16);
+  const unsigned w_row = lds32 + OFF_WST + (ot * 32 + lr) * WPITCH_S + lh * 16;
   const float al = a.alpha[ot * 32 + lr], be = a.beta[ot * 32 + lr];
+  // the ring starts zeroed: a kh = 7 byte row (zero weight) read before its
+  // first write must hold a valid code (an e4m3 NaN times 0 is NaN)
+  for (int i = tid; i < CR_SLOTS * CR_ROW / 16; i += SNW * 64) *(v4i*)(lds + OFF_CR + i * 16) = v4i{0, 0, 0, 0};
   __syncthreads();
   // A-row permutation: lane row i -> conv column offset pi(i) (D reg r of half h = column 16h + r)
   const int pi = ((lr >> 3) << 2) + (lr & 3) + 16 * ((lr >> 2) & 1);
-  const int a_unit = 28 * q + 1 + pi;  // super-col unit of tap kx = 0 (unit = super col + 4)
-  int8_t* stg = lds + OFF_STAGE + wave * 512;
+  const int ox = 28 * q - 1 + pi;  // this lane's conv column
+  // k-step t, lane half lh reads unit (c = t >> 1, j = 2 (t & 1) + lh): super col ox - 2 + j
+  const unsigned a_col = lds32 + OFF_CR + (unsigned)(ox + 2 + lh) * 16;
+  int8_t* stg = lds + OFF_STAGE + wave * STG;
+
+  // converter lanes: (input row r of the quad, unit u): a wave = 16 units x 4 rows
+  const int cv_r = (tid >> 4) & 3, cv_u = (tid & 15) + 16 * (tid >> 6);
 
   ST_DECL;
   for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
     const int n = item / a.nb, band = item - n * a.nb;
     const int py0 = band * a.R, py1 = min(56, py0 + a.R);
     if (py0 >= py1) continue;
-    const int sr0 = 2 * py0 - 3;  // first super row (pair k = super rows sr0+2k, sr0+2k+1)
+    // quad k = input rows iy0 + 4k .. + 3 (iy0 = 4 py0 - 5); step t converts
+    // quad t + 3 = rows 4p + 7 .. 4p + 10 (conv rows 2p + 2 .. 2p + 6) while it
+    // reads conv rows 2p, 2p + 1, whose last rows came with quad t + 2
+    const int iy0 = 4 * py0 - 5;
     const float* img = a.x + (size_t)n * 3 * 224 * 224;
 
-    // Super-row pair k = super rows sr0+2k, sr0+2k+1.  Thread = (pixel row
-    // dy, super row h of the pair, unit): unit = super col + 4 (units 0..3
-    // and 116..127 are the zero border); its input = channels 0..2 x pixels
-    // (2 sc, 2 sc + 1) of image row 2 sr + dy: three float2 loads.  Pair k's
-    // loads sit in register set k % (PD + 1) (compile-time: the step loop is
-    // unrolled by PD + 1) until convert_pair quantises them into the patch.
-    const int cv_unit = tid & 127, cv_h = (tid >> 7) & 1, cv_dy = tid >> 8, cv_sc = cv_unit - 4;
     using F2 = float __attribute__((ext_vector_type(2)));
     F2 raw[PD + 1][3];
-    auto load_pair = [&](int k, F2 (&r)[3]) {
-      const int sr = sr0 + 2 * k + cv_h;
-      if ((unsigned)sr < 112u && (unsigned)cv_sc < 112u) {
-        const float* src = img + (size_t)(2 * sr + cv_dy) * 224 + 2 * cv_sc;
+    auto load_quad = [&](int k, F2 (&r)[3]) {
+      const int iy = iy0 + 4 * k + cv_r, sc = cv_u - 4;
+      if ((unsigned)iy < 224u && (unsigned)sc < 112u) {
+        const float* src = img + (size_t)iy * 224 + 2 * sc;
 #pragma unroll
         for (int c = 0; c < 3; ++c) r[c] = *(const F2*)(src + (size_t)c * 224 * 224);
       } else {
@@ -149,94 +169,93 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
         for (int c = 0; c < 3; ++c) r[c] = F2{0.f, 0.f};
       }
     };
-    // Quantise pair k into two super rows of the patch ring: each thread
-    // writes the 8 bytes of its dy (dx = 0, 1) of one super-pixel.
-    auto convert_pair = [&](int k, const F2 (&r)[3]) {
-      const int sr = sr0 + 2 * k + cv_h;
-      int2 out = {0, 0};
-      if ((unsigned)sr < 112u && (unsigned)cv_sc < 112u) {
-        if constexpr (F8) {  // (c0, c1, c2, +0) e4m3 per pixel
-          out.x = (int)enc4_f8(r[0][0] * a.inv_s, r[1][0] * a.inv_s, r[2][0] * a.inv_s, 0.f, -448.f);
-          out.y = (int)enc4_f8(r[0][1] * a.inv_s, r[1][1] * a.inv_s, r[2][1] * a.inv_s, 0.f, -448.f);
-        } else {
-          unsigned u[3][2];  // [c][dx]: clamp(x/s) + 1.5*2^23 -> rne'd int8 in the low byte
+    // Quantise quad k and scatter each pixel pair into the 4 conv rows oy whose
+    // window 2oy-3 .. 2oy+4 holds its input row iy (kh = iy - 2oy + 3).  Rows
+    // of conv rows outside the band land in slots that the band's own rows
+    // overwrite before they are read (tools: the stem parity tests at 1..14
+    // bands per image).
+    auto convert_quad = [&](int k, const F2 (&r)[3]) {
+      const int iy = iy0 + 4 * k + cv_r;
+      unsigned v[3];
 #pragma unroll
-          for (int c = 0; c < 3; ++c)
-#pragma unroll
-            for (int dx = 0; dx < 2; ++dx)
-              u[c][dx] = __float_as_uint(__builtin_amdgcn_fmed3f(r[c][dx] * a.inv_s, -127.f, 127.f) + 12582912.0f);
-#pragma unroll
-          for (int dx = 0; dx < 2; ++dx) {  // bytes (c0, c1, c2, 0)
-            const unsigned t = __builtin_amdgcn_perm(u[1][dx], u[0][dx], 0x0c0c0400u);
-            (dx ? out.y : out.x) = (int)__builtin_amdgcn_perm(u[2][dx], t, 0x0c040100u);
-          }
+      for (int c = 0; c < 3; ++c) {
+        if constexpr (F8) {  // e4m3 codes of the two pixels; padding quantises to +0
+          const float c0 = __builtin_amdgcn_fmed3f(r[c][0] * a.inv_s, -448.f, 448.f) + 0.0f;
+          const float c1 = __builtin_amdgcn_fmed3f(r[c][1] * a.inv_s, -448.f, 448.f) + 0.0f;
+          v[c] = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(c0, c1, 0, false);
+        } else {  // clamp(x/s) + 1.5*2^23 -> rne'd int8 in the low byte
+          const unsigned u0 = __float_as_uint(__builtin_amdgcn_fmed3f(r[c][0] * a.inv_s, -127.f, 127.f) + 12582912.0f);
+          const unsigned u1 = __float_as_uint(__builtin_amdgcn_fmed3f(r[c][1] * a.inv_s, -127.f, 127.f) + 12582912.0f);
+          v[c] = __builtin_amdgcn_perm(u1, u0, 0x0c0c0400u);
         }
       }
-      *(int2*)(lds + OFF_PATCH + (sr & (PATCH_SLOTS - 1)) * PATCH_ROW + cv_unit * 16 + cv_dy * 8) = out;
-    };
-    // One conv row (global row oy): the wave's 32 px x 32 oc tile, 8 k-steps.
-    // int8: fragments stream two k-steps ahead through a 3-deep ring of
-    // untracked ds_read_b128 (inline asm: the compiler can neither hoist all
-    // 16 reads nor keep them all live -- two workgroups share the registers).
-    const unsigned a_col = lds32 + OFF_PATCH + (a_unit + lh) * 16;
-    const unsigned w_row = lds32 + (unsigned)(wlds - lds);
-    auto conv_row = [&](int oy) {
-      Acc acc = Acc{0};
-      unsigned ra[4];  // super rows oy-2 .. oy+1 (ky = 0..3)
+      const int oyb = (iy - 3) >> 1;  // ceil((iy - 4) / 2): the first of the 4 conv rows
 #pragma unroll
-      for (int ky = 0; ky < 4; ++ky) ra[ky] = a_col + ((oy - 2 + ky) & (PATCH_SLOTS - 1)) * PATCH_ROW;
-      if constexpr (F8) {  // k-steps 2kp, 2kp+1 = the two halves of one 64-deep fp8 MFMA
-        v4i fa[2][2], fw[2][2];
-#define STEM_RD8(kp)                                                                                              \
-  asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(fa[(kp) & 1][0]) : "v"(ra[kp]) : "memory");                   \
-  asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(fa[(kp) & 1][1]) : "v"(ra[kp]) : "memory");                  \
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fw[(kp) & 1][0]) : "v"(w_row), "n"(64 * (kp)) : "memory");  \
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fw[(kp) & 1][1]) : "v"(w_row), "n"(64 * (kp) + 32) : "memory")
-#define STEM_K8(kp)                                                                                               \
-  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(fa[(kp) & 1][0]), "+v"(fa[(kp) & 1][1]), "+v"(fw[(kp) & 1][0]),        \
-               "+v"(fw[(kp) & 1][1]) : "n"((kp) + 1 < 4 ? 4 : 0) : "memory");                                     \
-  acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(cat8(fa[(kp) & 1][0], fa[(kp) & 1][1]),                       \
-                                                        cat8(fw[(kp) & 1][0], fw[(kp) & 1][1]), acc, 0, 0, 0, 0, 0, 0)
-        STEM_RD8(0);
-        STEM_RD8(1);
-        STEM_K8(0);
-        STEM_RD8(2);
-        STEM_K8(1);
-        STEM_RD8(3);
-        STEM_K8(2);
-        STEM_K8(3);
-#undef STEM_RD8
-#undef STEM_K8
-      } else {
-        v4i fa[3], fw[3];
-#define STEM_RD(kk)                                                                                    \
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[(kk) % 3]) : "v"(ra[(kk) >> 1]), "n"(32 * ((kk) & 1)) \
-               : "memory");                                                                          \
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fw[(kk) % 3]) : "v"(w_row), "n"(32 * (kk)) : "memory")
-#define STEM_K(kk)                                                                                     \
-  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(fa[(kk) % 3]), "+v"(fw[(kk) % 3]) : "n"((kk) + 1 < 8 ? 2 : 0)    \
-               : "memory");                                                                          \
-  acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[(kk) % 3], fw[(kk) % 3], acc, 0, 0, 0)
+      for (int e = 0; e < 4; ++e) {
+        const int oyc = oyb + e, kh = iy - 2 * oyc + 3;
+        int8_t* dst = lds + OFF_CR + (oyc & (CR_SLOTS - 1)) * CR_ROW + cv_u * 16 + 2 * kh;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) *(unsigned short*)(dst + c * CR_PLANE) = (unsigned short)v[c];
+      }
+    };
+    // One conv row (global row oy): the wave's 32 px x 64 oc (two tiles), 6
+    // k-steps; A fragments stream through a 3-deep ring of untracked
+    // ds_read_b128 (inline asm: completion by explicit lgkmcnt waits).
+    auto conv_row = [&](int oy) {
+      Acc c0 = Acc{0};
+      const unsigned ra = a_col + (oy & (CR_SLOTS - 1)) * CR_ROW;
+      v4i fa[3];
+      v4i fw[3];
+#define STEM_RD(t)                                                                                               \
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[(t) % 3]) : "v"(ra), "n"(((t) >> 1) * CR_PLANE + ((t) & 1) * 32) \
+               : "memory");                                                                                      \
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fw[(t) % 3]) : "v"(w_row), "n"(32 * (t)) : "memory")
+#define STEM_WAIT(t, n) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(fa[(t) % 3]), "+v"(fw[(t) % 3]) : "n"(n) : "memory")
+      if constexpr (F8) {  // k-steps 2i, 2i+1 = the two halves of one 64-deep fp8 MFMA
+#define STEM_K8(i)                                                                                      \
+  c0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(cat8(fa[(2 * (i)) % 3], fa[(2 * (i) + 1) % 3]),  \
+                                                       cat8(fw[(2 * (i)) % 3], fw[(2 * (i) + 1) % 3]), c0, 0, 0, 0, 0, 0, 0)
         STEM_RD(0);
         STEM_RD(1);
+        STEM_WAIT(0, 2);
+        STEM_WAIT(1, 0);
+        STEM_K8(0);
+        STEM_RD(2);
+        STEM_RD(3);
+        STEM_WAIT(2, 2);
+        STEM_WAIT(3, 0);
+        STEM_K8(1);
+        STEM_RD(4);
+        STEM_RD(5);
+        STEM_WAIT(4, 2);
+        STEM_WAIT(5, 0);
+        STEM_K8(2);
+#undef STEM_K8
+      } else {
+#define STEM_K(t) c0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[(t) % 3], fw[(t) % 3], c0, 0, 0, 0)
+        STEM_RD(0);
+        STEM_RD(1);
+        STEM_WAIT(0, 2);
         STEM_K(0);
         STEM_RD(2);
+        STEM_WAIT(1, 2);
         STEM_K(1);
         STEM_RD(3);
+        STEM_WAIT(2, 2);
         STEM_K(2);
         STEM_RD(4);
+        STEM_WAIT(3, 2);
         STEM_K(3);
         STEM_RD(5);
+        STEM_WAIT(4, 2);
         STEM_K(4);
-        STEM_RD(6);
+        STEM_WAIT(5, 0);
         STEM_K(5);
-        STEM_RD(7);
-        STEM_K(6);
-        STEM_K(7);
-#undef STEM_RD
 #undef STEM_K
       }
-      return acc;
+#undef STEM_RD
+#undef STEM_WAIT
+      return c0;
     };
     auto mx3 = [](Pv x, Pv y, Pv z) -> Pv {
       if constexpr (F8)
@@ -248,7 +267,7 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
     // Horizontal 3-max of a conv row, H[m] = max(local cols 2m, 2m+1, 2m+2):
     // half 0 takes column 16 from half 1; quarter 0's column 0 is conv column
     // -1 (pool padding).  Half 1's H[6], H[7] and half 0's beyond m=7 are unused.
-    auto hpool = [&](Acc c, Pv (&H)[8]) {
+    auto hpool = [&](const Acc& c, Pv (&H)[8]) {
       unsigned x0 = __builtin_bit_cast(unsigned, c[0]), c16 = x0;
       swap32(x0, c16);  // lanes 0-31: c16 = lanes 32-63's c[0]
       const Pv c0v = (q == 0 && lh == 0) ? kLow : c[0];
@@ -258,18 +277,18 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
       H[7] = mx3(c[14], c[15], __builtin_bit_cast(Pv, c16));
     };
 
-    // ---- prologue: pairs 0..2 converted (super rows 2py0-3 .. 2py0+2),
-    // pairs 3 .. 2+PD loaded; H of conv row 2py0-1.
-    static_assert(PD == 2, "prologue ring assignment below assumes 3 register sets");
-    load_pair(0, raw[0]);
-    load_pair(1, raw[1]);
-    load_pair(2, raw[2]);
-    convert_pair(0, raw[0]);
-    load_pair(3, raw[0]);
-    convert_pair(1, raw[1]);
-    load_pair(4, raw[1]);
-    convert_pair(2, raw[2]);
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): patch rows written (loads stay in flight)
+    // ---- prologue: quads 0..2 converted (input rows 4py0-5 .. 4py0+6),
+    // quads 3 .. 2+PD loaded (quad k in register set k % (PD + 1)); H of
+    // conv row 2py0-1.
+    static_assert(PD >= 2, "the prologue converts quads 0..2 from their own sets");
+#pragma unroll
+    for (int k = 0; k <= PD; ++k) load_quad(k, raw[k]);
+    convert_quad(0, raw[0]);
+    load_quad(PD + 1, raw[0]);
+    convert_quad(1, raw[1]);
+    load_quad(PD + 2, raw[1]);
+    convert_quad(2, raw[2]);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): ring rows written (loads stay in flight)
     __builtin_amdgcn_s_barrier();
     Pv Hp[8];
     if (py0 == 0) {
@@ -287,20 +306,20 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
       const v4i o = *(const v4i*)(stg + pxl * 32 + hf * 16);
       if (lane < 28) *(v4i*)(a.y + (((size_t)n * 56 + p) * 56 + 14 * q + pxl) * 64 + ot * 32 + hf * 16) = o;
     };
-    // step t (pooled row p = py0 + t): pair t+3 (register set (t+3) % 3 =
-    // t % 3) is quantised for the next step, pair t+5 is loaded into the set
-    // pair t+2 freed, conv rows 2p and 2p+1 are computed and pooled.
+    // step t (pooled row p = py0 + t): quad t+3 (register set (t+3) % (PD+1))
+    // is quantised for the next step, quad t+3+PD is loaded into the set quad
+    // t+2 freed, conv rows 2p and 2p+1 are computed and pooled.
     auto step = [&](int t, auto setc) {
-      constexpr int S = decltype(setc)::value;  // == t % 3
+      constexpr int S = decltype(setc)::value;  // == t % (PD + 1)
       const int p = py0 + t;
       ST(5);
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): last step's patch rows and staging
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): last step's ring rows and staging
       __builtin_amdgcn_s_barrier();
       ST(0);
-      convert_pair(t + 3, raw[S]);
+      convert_quad(t + 3, raw[(S + 3) % (PD + 1)]);
       ST(1);
       if (t > 0) store_row(p - 1);
-      load_pair(t + 5, raw[(S + 2) % 3]);
+      load_quad(t + 3 + PD, raw[(S + 2) % (PD + 1)]);
       ST(2);
 
       Pv He[8], Ho[8];
@@ -325,14 +344,24 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
       ST(4);
     };
     const int nsteps = py1 - py0;
+    static_assert(PD == 4, "the step loop below is unrolled by PD + 1 = 5");
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
     int t = 0;
-    for (; t + 3 <= nsteps; t += 3) {
-      step(t, std::integral_constant<int, 0>{});
-      step(t + 1, std::integral_constant<int, 1>{});
-      step(t + 2, std::integral_constant<int, 2>{});
+    for (; t + 5 <= nsteps; t += 5) {
+      step(t, I0{});
+      step(t + 1, I1{});
+      step(t + 2, I2{});
+      step(t + 3, I3{});
+      step(t + 4, I4{});
     }
-    if (t < nsteps) step(t, std::integral_constant<int, 0>{});
-    if (t + 1 < nsteps) step(t + 1, std::integral_constant<int, 1>{});
+    if (t < nsteps) step(t, I0{});
+    if (t + 1 < nsteps) step(t + 1, I1{});
+    if (t + 2 < nsteps) step(t + 2, I2{});
+    if (t + 3 < nsteps) step(t + 3, I3{});
     if (py1 > py0) store_row(py1 - 1);
     wait_vm0();
     __syncthreads();  // ring reuse by the next item
@@ -353,48 +382,38 @@ int num_cus_stem() {
 
 }  // namespace
 
-size_t stem_packed_bytes() { return 64 * 256; }
+size_t stem_packed_bytes() { return 64 * SK; }
 
-// OIHW int8 q[64][3][7][7] -> [64][ky 4][kx 4][dy 2][dx 2][c 4] with
-// kh = 2ky+dy-1, kw = 2kx+dx-1; rows of channels with alpha < 0 are negated
-// and |alpha| returned, which keeps the fused stem's pool-before-epilogue exact.
-void pack_stem_weights(const int8_t* q, const float* alpha, int8_t* out, float* alpha_abs) {
-  for (int i = 0; i < 64 * 256; ++i) out[i] = 0;
+// OIHW q[64][3][7][7] -> [64 oc][t 6][lh 2][16 B]: unit m = 2t + lh is
+// (c = m >> 2, j = m & 3), byte b = 2 kh + dx is tap (kh, kw = 2j + dx - 1);
+// kw = -1 and kh = 7 are zero (the K order of stem_fused_kernel's A
+// fragments).  Rows of channels with alpha < 0 are negated and |alpha|
+// returned, which keeps the fused stem's pool-before-epilogue exact.
+template <typename T, typename Neg>
+void pack_stem(const T* q, const float* alpha, T* out, float* alpha_abs, Neg neg_of) {
+  for (int i = 0; i < 64 * SK; ++i) out[i] = 0;
   for (int o = 0; o < 64; ++o) {
     const bool neg = alpha[o] < 0.f;
     alpha_abs[o] = neg ? -alpha[o] : alpha[o];
-    for (int ky = 0; ky < 4; ++ky)
-      for (int kx = 0; kx < 4; ++kx)
-        for (int dy = 0; dy < 2; ++dy)
-          for (int dx = 0; dx < 2; ++dx) {
-            const int kh = 2 * ky + dy - 1, kw = 2 * kx + dx - 1;
-            if (kh < 0 || kw < 0) continue;
-            for (int c = 0; c < 3; ++c) {
-              const int v = q[((o * 3 + c) * 7 + kh) * 7 + kw];
-              out[o * 256 + (((ky * 4 + kx) * 2 + dy) * 2 + dx) * 4 + c] = (int8_t)(neg ? -v : v);
-            }
-          }
+    for (int m = 0; m < 12; ++m) {
+      const int c = m >> 2, j = m & 3;
+      for (int b = 0; b < 16; ++b) {
+        const int kh = b >> 1, kw = 2 * j + (b & 1) - 1;
+        if (kh > 6 || kw < 0 || kw > 6) continue;
+        const T v = q[((o * 3 + c) * 7 + kh) * 7 + kw];
+        out[o * SK + m * 16 + b] = neg ? neg_of(v) : v;
+      }
+    }
   }
+}
+
+void pack_stem_weights(const int8_t* q, const float* alpha, int8_t* out, float* alpha_abs) {
+  pack_stem(q, alpha, out, alpha_abs, [](int8_t v) { return (int8_t)-v; });
 }
 
 // e4m3 twin: the sign bit is the negation.
 void pack_stem_weights_f8(const uint8_t* q, const float* alpha, uint8_t* out, float* alpha_abs) {
-  for (int i = 0; i < 64 * 256; ++i) out[i] = 0;
-  for (int o = 0; o < 64; ++o) {
-    const bool neg = alpha[o] < 0.f;
-    alpha_abs[o] = neg ? -alpha[o] : alpha[o];
-    for (int ky = 0; ky < 4; ++ky)
-      for (int kx = 0; kx < 4; ++kx)
-        for (int dy = 0; dy < 2; ++dy)
-          for (int dx = 0; dx < 2; ++dx) {
-            const int kh = 2 * ky + dy - 1, kw = 2 * kx + dx - 1;
-            if (kh < 0 || kw < 0) continue;
-            for (int c = 0; c < 3; ++c) {
-              const uint8_t v = q[((o * 3 + c) * 7 + kh) * 7 + kw];
-              out[o * 256 + (((ky * 4 + kx) * 2 + dy) * 2 + dx) * 4 + c] = neg ? (uint8_t)(v ^ 0x80) : v;
-            }
-          }
-  }
+  pack_stem(q, alpha, out, alpha_abs, [](uint8_t v) { return (uint8_t)(v ^ 0x80); });
 }
 
 hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float* alpha, const float* beta,

@@ -22,7 +22,7 @@ __global__ void fill_rand(int8_t* p, size_t n, unsigned seed) {
 int main(int argc, char** argv) {
   const int W = argc > 1 ? atoi(argv[1]) : 7;
   const int dbg = argc > 2 ? atoi(argv[2]) : 0;
-  const int C = W == 7 ? 512 : W == 14 ? 256 : 128, N = 256, P = N * W * W;
+  const int C = W == 7 ? 512 : W == 14 ? 256 : 128, N = argc > 3 ? atoi(argv[3]) : 256, P = N * W * W;
   int8_t *x, *w, *res, *y;
   float *al, *be;
   const size_t wb = (size_t)C * (C / 32) * 304;
