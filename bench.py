@@ -109,20 +109,23 @@ class GatherPipeline:
 
 
 def pmc_traffic(kernel_family):
-    """HBM bytes per launch of a kernel family from the committed rocprofv3 PMC
-    summary (profiles/*pmc_traffic.json, written by tools/pmc_traffic.py:
-    FETCH_SIZE doubled per MI355X_MICROARCH.md + WRITE_SIZE), or None."""
+    """(HBM bytes per launch, source) of a kernel family from the newest
+    committed rocprofv3 PMC summary (profiles/*pmc_traffic.json, written by
+    tools/pmc_traffic.py from separate --pmc passes of tools/measure.sh:
+    FETCH_SIZE doubled per MI355X_MICROARCH.md + WRITE_SIZE) -- NOT measured in
+    this run (counters need their own rocprofv3 passes) -- or (None, None)."""
     import glob
     paths = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                                           "*pmc_traffic.json")))
     if not paths:
-        return None
+        return None, None
     try:
         data = json.load(open(paths[-1]))
         ent = data.get("families", {}).get(kernel_family)
-        return None if ent is None else ent["hbm_bytes_per_launch"]
+        src = "committed profile " + os.path.relpath(paths[-1], os.path.dirname(os.path.abspath(__file__)))
+        return (None, None) if ent is None else (ent["hbm_bytes_per_launch"], src)
     except Exception:
-        return None
+        return None, None
 
 
 def host_threads():
@@ -381,7 +384,7 @@ def main():
     dom_per_fwd = fam_n[dom] / max(n_fwd, 1)
     ops_per_launch = 2.0 * fam_macs[dom] * B / max(dom_per_fwd, 1e-9)
     achieved = ops_per_launch / (dom_avg_us * 1e-6) / 1e12 if dom_avg_us > 0 else 0.0
-    traffic = pmc_traffic(FAMILIES[dom])
+    traffic, traffic_src = pmc_traffic(FAMILIES[dom])
 
     metric = "images/sec ResNet-18 int8 batch=256 @1/2/4/8 GPU; int8 GEMM TOPS vs peak"
     workload = ("ResNet-18 int8 224x224, batch 256 per GPU (BASELINE configs[2]; "
@@ -411,6 +414,7 @@ def main():
                      "achieved": round(achieved, 1), "peak": round(PEAK_I8_TOPS, 1),
                      "unit": "TFLOP/s", "int8_ops": not fp8,
                      "frac": round(achieved / PEAK_I8_TOPS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "ops_per_launch": ops_per_launch, "avg_launch_us": round(dom_avg_us, 2),
                      "launches_timed": fam_n[dom], "timing": "hipEvents on the forward's stream around "
                      "every launch (separate pass of prof_steps forwards after the timed region), "

@@ -55,6 +55,15 @@ def _step(v):
     return 2.0 ** (np.floor(np.log2(v)) - 3)
 
 
+# Fraction of e4m3 codes that may differ from the oracle's exact-sum result,
+# per kind: 1.5x the largest fraction measured over this file's cases on
+# gfx950 (round 3: 3x3 convs 1.6e-4 .. 4.8e-4, 1x1/s2 downsamples 6.5e-4 ..
+# 1.04e-3, stem 5.5e-5 .. 2.3e-4; the MFMA results are deterministic, so the
+# measured fractions are exact for these seeds).  Round 2's bar was 3e-3 for
+# all kinds.
+F8_FRAC = {"conv": 7.5e-4, "ds": 1.6e-3, "stem": 3.5e-4}
+
+
 def _check_conv(got, ref, err_bound, frac, what):
     a, b = O.decode_f8(got).astype(np.float64), O.decode_f8(ref).astype(np.float64)
     lim = _step(np.maximum(np.abs(a), np.abs(b))) + 2 * err_bound
@@ -142,7 +151,7 @@ def _run_conv(shape, residual, N):
     assert len(np.unique(ref)) > 50  # a real spread of codes, not a saturated tensor
     s_abs = O.conv_f8_acc(x & 0x7F, wq & 0x7F, s, p)  # exact sum |w x|
     err = 2.0 ** -16 * np.abs(alpha).astype(np.float64)[None, :, None, None] * s_abs
-    _check_conv(got, ref, err, 3e-3, name)
+    _check_conv(got, ref, err, F8_FRAC["ds" if k == 1 else "conv"], name)
 
 
 def _maxpool_f64(a):
@@ -180,7 +189,7 @@ def test_stem_fused_f8_within_bound(gpu, N):
     got = nhwc_to_nchw(y.cpu().numpy())
     assert got.shape == ref.shape
     assert len(np.unique(ref)) > 50
-    _check_conv(got, ref, err, 3e-3, "stem")
+    _check_conv(got, ref, err, F8_FRAC["stem"], "stem")
 
 
 @pytest.mark.parametrize("N,grid", [(3, None), (5, "2")])
@@ -240,7 +249,7 @@ def test_s2_conv_with_fused_downsample_f8(gpu, C, H, N):
         assert len(np.unique(r)) > 50
         s_abs = O.conv_f8_acc(x & 0x7F, wqq & 0x7F, s_, p_)
         err = 2.0 ** -16 * np.abs(al).astype(np.float64)[None, :, None, None] * s_abs
-        _check_conv(g, r, err, 3e-3, what)
+        _check_conv(g, r, err, F8_FRAC["ds" if what == "ds" else "conv"], what)
     alone = ops.conv2d_nhwc_f8(xd, wdev, OC, 3, 2, 1, _cuda(alpha), _cuda(beta), relu=True).cpu().numpy()
     assert np.array_equal(y.cpu().numpy(), alone)
 
