@@ -12,6 +12,9 @@ HDR = include/dlq.h dlq_amd/csrc/dlq_internal.h dlq_amd/csrc/device_common.h
 
 all: dlq_amd/libdlq.so bin/dlq_e2e oracle
 
+# the layer1 block interleaves its epilogue FMAs with MFMAs: keep them scalar
+build/block_l1.o: HIPFLAGS += -fno-slp-vectorize
+
 build/%.o: dlq_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<

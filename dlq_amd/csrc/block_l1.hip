@@ -467,6 +467,15 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
 // edge (each job reads its own first two k-steps); the residual is a
 // compiler-tracked load (conv2 waves issue no LDS-DMA, so the compiler's
 // vmcnt arithmetic is exact for them).
+// The requantisation runs between the MFMAs of the next job: scalar FMAs
+// (device_common.h epi4_relu_s); -DDLQ_L1_PACKED keeps the packed forms.
+#ifdef DLQ_L1_PACKED
+#define DLQ_L1_EPI epi4_relu
+#define DLQ_L1_EPI_RES epi4_res_relu
+#else
+#define DLQ_L1_EPI epi4_relu_s
+#define DLQ_L1_EPI_RES epi4_res_relu_s
+#endif
 template <bool SECOND>
 __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds, unsigned lds32, int wave, int rows,
                                                  int nphase) {
@@ -524,9 +533,9 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
   auto epi_group = [&](const v16i& acc, int g4, const unsigned (&rg)[4]) -> unsigned {
     const int ac[4] = {acc[4 * g4], acc[4 * g4 + 1], acc[4 * g4 + 2], acc[4 * g4 + 3]};
     if constexpr (SECOND)
-      return epi4_res_relu(ac, al + 4 * g4, be + 4 * g4, rg[g4], a.s_res);
+      return DLQ_L1_EPI_RES(ac, al + 4 * g4, be + 4 * g4, rg[g4], a.s_res);
     else
-      return epi4_relu(ac, al + 4 * g4, be + 4 * g4);
+      return DLQ_L1_EPI(ac, al + 4 * g4, be + 4 * g4);
   };
   // store layout -> MFMA layout
   auto res_regs = [&](const v4i& rs, unsigned (&rg)[4]) {
