@@ -131,100 +131,114 @@ __global__ __launch_bounds__(64) void linear_kernel(const int8_t* __restrict__ x
 // gap_fc_kernel: the network head (GAP + FC, RK/runtime/infer_e2e.cu:417-433)
 // in ONE launch for C = K = 512, fp32 logits -- the same integers and the same
 // float ops as gap16_kernel followed by linear_kernel<1>, so the logits are
-// bit-identical.  Workgroup = GF images x 256 output channels (grid GF-image
-// groups x 4: 256 workgroups at B = 256; the four workgroups of an image group
-// have block ids 64 apart, i.e. the same XCD, so they share its L2 copy of the
-// activations).  Phase 1: one wave per image, lane = (pixel parity, 16-channel
-// group): a wave's load is 2 whole 512-byte pixel rows, every load of the
-// image issued before the first sum, one v_permlane32_swap per sum joins the
-// two parities; the int8 GAP codes go to LDS.  The first output tile's weight
-// fragments are loaded before the activations, the second's behind them.
-// Phase 2: each wave runs linear_kernel's MFMA loop for its two 32-channel
-// tiles (two independent accumulator chains) with the B fragments read from
-// LDS (lanes lr >= GF read a duplicate row; their D columns are not stored).
-constexpr int GF = 4;        // images per workgroup (one per wave)
-constexpr int GF_PR = 28;    // pixel loads per lane: HW <= 2 * GF_PR
-constexpr int GF_OCW = 256;  // output channels per workgroup (4 waves x 2 tiles)
+// bit-identical.  Workgroup = GF images x 256 output channels, 8 waves (grid
+// GF-image groups x 4: 256 workgroups at B = 256; the four workgroups of an
+// image group have block ids 64 apart, i.e. the same XCD, so they share its
+// L2 copy of the activations).  The head is latency-bound (6.4 MB in, 0.26
+// GOP): every wave issues ALL its loads first -- its output tile's 16 weight
+// fragments, the epilogue constants of its 16 outputs per lane, then its
+// share of the activations -- so it waits for memory once.
+//   Phase 1: wave w sums half (w & 1) of image w >> 1's pixels; lane =
+//   (pixel parity, 16-channel group), one v_permlane32_swap joins the
+//   parities; the halves meet as int32 partial sums in LDS, then the int8
+//   GAP codes (clamp(rne(float(sum) * k))) go to LDS.
+//   Phase 2: wave w runs linear_kernel's MFMA loop for output tile w of the
+//   workgroup's 256 channels, B fragments from LDS (lanes lr >= GF read a
+//   duplicate row; their D columns are not stored).
+constexpr int GF = 4;        // images per workgroup
+constexpr int GF_PL = 14;    // pixel loads per lane: HW <= 4 * GF_PL (two waves x two parities)
+constexpr int GF_OCW = 256;  // output channels per workgroup (8 waves x 1 tile)
 
-__global__ __launch_bounds__(256) void gap_fc_kernel(const int8_t* __restrict__ x, int N, int HW, float k,
+__global__ __launch_bounds__(512) void gap_fc_kernel(const int8_t* __restrict__ x, int N, int HW, float k,
                                                      const int8_t* __restrict__ w, int OC, int OCp,
                                                      const float* __restrict__ alpha, const float* __restrict__ beta,
                                                      float* __restrict__ y) {
   constexpr int C = 512, NK = C / 32;
   __shared__ __attribute__((aligned(16))) int8_t g[GF * C];
+  __shared__ __attribute__((aligned(16))) int part[GF][C];  // the second half's partial sums
+  __shared__ __attribute__((aligned(16))) float eab_s[2 * GF_OCW];  // alpha, beta of the workgroup's outputs
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, lr = lane & 31, lh = lane >> 5;
   const int n0 = blockIdx.x * GF;
   const size_t wstride = (size_t)(OCp / 64) * 64 * 64;
-  const int ot0 = (blockIdx.y * GF_OCW) / 32 + wv * 2;  // this wave's tiles ot0, ot0 + 1
-  auto load_w = [&](int ot, v4i (&a)[NK]) {
+  const int ot = (blockIdx.y * GF_OCW) / 32 + wv;  // this wave's output tile
+  // 1. loads in the order of need (vmcnt counts in issue order): this
+  // wave's activations, the output tile's weight fragments, the epilogue
+  // constants of its 16 outputs per lane
+  const int img = wv >> 1, half = wv & 1, cg = lane & 31, par = lane >> 5;
+  const int hh = (HW + 1) >> 1, p0 = half * hh, p1 = half ? HW : hh;  // this wave's pixels [p0, p1)
+  const int n = min(n0 + img, N - 1);  // a short last group re-reads a valid image
+  const int8_t* src = x + (size_t)n * HW * C + cg * 16;
+  v4i v[GF_PL];
+#pragma unroll
+  for (int j = 0; j < GF_PL; ++j) v[j] = *(const v4i*)(src + (size_t)min(p0 + par + 2 * j, HW - 1) * C);
+  v4i a0[NK];
+  {
     const int oc = min(ot * 32, OCp - 32) + lr, ol = oc & 63, sw = (ol >> 2) & 3;
     const int8_t* wp = w + ((size_t)(oc >> 6) * 64 + ol) * 64;
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk)
-      a[kk] = *(const v4i*)(wp + (size_t)(kk >> 1) * wstride + ((((2 * kk + lh) & 3) ^ sw) << 4));
-  };
-  v4i a0[NK], a1[NK];
-  load_w(ot0, a0);
-  {
-    const int cg = lane & 31, par = lane >> 5;
-    const int n = min(n0 + wv, N - 1);  // a short last group re-reads a valid image
-    const int8_t* src = x + (size_t)n * HW * C + cg * 16;
-    v4i v[GF_PR];
+      a0[kk] = *(const v4i*)(wp + (size_t)(kk >> 1) * wstride + ((((2 * kk + lh) & 3) ^ sw) << 4));
+  }
+  // the workgroup's 256 alpha / beta: one of each per thread, through LDS
+  const int oe = min(blockIdx.y * GF_OCW + (t & (GF_OCW - 1)), OC - 1);
+  const float eab = t < GF_OCW ? alpha[oe] : beta[oe];
+  __builtin_amdgcn_sched_barrier(0);  // every load above is issued before the first sum
+  int s[16];
 #pragma unroll
-    for (int j = 0; j < GF_PR; ++j) v[j] = *(const v4i*)(src + (size_t)min(par + 2 * j, HW - 1) * C);
-    load_w(ot0 + 1, a1);
-    int s[16];
+  for (int e = 0; e < 16; ++e) s[e] = 0;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) s[e] = 0;
+  for (int j = 0; j < GF_PL; ++j) {
+    const bool ok = p0 + par + 2 * j < p1;
 #pragma unroll
-    for (int j = 0; j < GF_PR; ++j) {
-      const bool ok = par + 2 * j < HW;
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int b = 0; b < 4; ++b) s[q * 4 + b] += ok ? (int)(signed char)(v[j][q] >> (8 * b)) : 0;
+  }
 #pragma unroll
-        for (int b = 0; b < 4; ++b) s[q * 4 + b] += ok ? (int)(signed char)(v[j][q] >> (8 * b)) : 0;
+  for (int e = 0; e < 16; ++e) {
+    unsigned lo = (unsigned)s[e], hi = (unsigned)s[e];
+    swap32(lo, hi);  // lanes 0-31: hi = the odd-pixel sum of the same channel group
+    s[e] += (int)hi;
+  }
+  eab_s[t] = eab;
+  if (half == 1 && par == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *(v4i*)(&part[img][cg * 16 + 4 * q]) = v4i{s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]};
+  }
+  __syncthreads();
+  if (half == 0 && par == 0) {  // exact int32 channel sums, then the GAP requantisation
+    v4i o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const v4i pp = *(const v4i*)(&part[img][cg * 16 + 4 * q]);
+      unsigned u = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) u |= ((unsigned)sat_rne((float)(s[q * 4 + b] + pp[b]) * k) & 0xffu) << (8 * b);
+      o[q] = (int)u;
     }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      unsigned lo = (unsigned)s[e], hi = (unsigned)s[e];
-      swap32(lo, hi);  // lanes 0-31: hi = the odd-pixel sum of the same channel group
-      s[e] += (int)hi;
-    }
-    if (par == 0) {
-      v4i o;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        unsigned u = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) u |= ((unsigned)sat_rne((float)s[q * 4 + b] * k) & 0xffu) << (8 * b);
-        o[q] = (int)u;
-      }
-      *(v4i*)(g + wv * C + cg * 16) = o;
-    }
+    *(v4i*)(g + img * C + cg * 16) = o;
   }
   __syncthreads();
 
+  // 2. FC tile ot: B fragments from LDS, two independent accumulation chains
   const int8_t* gb = g + (lr & (GF - 1)) * C + lh * 16;
   v16i acc0 = v16i{0}, acc1 = v16i{0};
 #pragma unroll
-  for (int kk = 0; kk < NK; ++kk) {
-    const v4i bf = *(const v4i*)(gb + kk * 32);
-    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[kk], bf, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[kk], bf, acc1, 0, 0, 0);
+  for (int kk = 0; kk < NK; kk += 2) {
+    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[kk], *(const v4i*)(gb + kk * 32), acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[kk + 1], *(const v4i*)(gb + (kk + 1) * 32), acc1, 0, 0, 0);
   }
+  const v16i acc = acc0 + acc1;
   const int r = n0 + lr;
-  if (lr >= GF || r >= N) return;
+  if (lr >= GF || r >= N || ot * 32 >= OC) return;
 #pragma unroll
-  for (int tt = 0; tt < 2; ++tt) {
-    const int ot = ot0 + tt;
-    const v16i& acc = tt ? acc1 : acc0;
+  for (int q = 0; q < 4; ++q) {
+    const int o0 = ot * 32 + 8 * q + 4 * lh, ol = o0 - blockIdx.y * GF_OCW;
+    const v4i a4 = *(const v4i*)(eab_s + ol), b4 = *(const v4i*)(eab_s + GF_OCW + ol);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int o0 = ot * 32 + 8 * q + 4 * lh;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (o0 + e < OC) y[(size_t)r * OC + o0 + e] = __builtin_fmaf((float)acc[4 * q + e], alpha[o0 + e], beta[o0 + e]);
-    }
+    for (int e = 0; e < 4; ++e)
+      if (o0 + e < OC)
+        y[(size_t)r * OC + o0 + e] = __builtin_fmaf((float)acc[4 * q + e], __int_as_float(a4[e]), __int_as_float(b4[e]));
   }
 }
 
@@ -464,10 +478,10 @@ hipError_t launch_mlp_fused(const float* x, int N, int in, int kp, float inv_s, 
 // C = K = 512, HW <= 56 (the ResNet-18 head); hipErrorInvalidValue otherwise.
 hipError_t launch_gap_fc(const int8_t* x, int N, int C, int HW, float k, const int8_t* w, int OC,
                          const float* alpha, const float* beta, float* y, hipStream_t s) {
-  if (C != 512 || HW < 1 || HW > 2 * GF_PR || N < 1 || OC < 1) return hipErrorInvalidValue;
+  if (C != 512 || HW < 1 || HW > 4 * GF_PL || N < 1 || OC < 1) return hipErrorInvalidValue;
   const int OCp = packed_oc(OC);
   const dim3 grid((N + GF - 1) / GF, (OC + GF_OCW - 1) / GF_OCW);
-  hipLaunchKernelGGL(gap_fc_kernel, grid, dim3(256), 0, s, x, N, HW, k, w, OC, OCp, alpha, beta, y);
+  hipLaunchKernelGGL(gap_fc_kernel, grid, dim3(512), 0, s, x, N, HW, k, w, OC, OCp, alpha, beta, y);
   return hipGetLastError();
 }
 
