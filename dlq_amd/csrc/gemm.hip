@@ -159,9 +159,14 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_generic_kernel(const int8
 
 
 // ---- aligned operands (K % 16 == 0, N % 16 == 0, 16-byte aligned bases):
-// both tiles stream by LDS-DMA through a 4-slot ring, three stages ahead.
-//  * A image: row m, 16-byte chunk c of its 64 K bytes at m*64 + 16*(c ^
-//    ((m >> 2) & 3)) -- a ds_read_b128 lane group's 16 rows hit 16 bank quads.
+// both tiles stream by LDS-DMA, K = 128 per stage through two slots.  Stage
+// s + 1 is issued right after the barrier that opens stage s (every wave has
+// left stage s - 1's slot by then), so its 64 KB land during stage s's 32
+// MFMAs per wave.  (A 4-slot ring of K = 64 stages, three ahead, measured
+// 6-12 % slower on one box: 8192^3 1547 vs 1646 TOPS, 4096^3 1648 vs 1852,
+// 50176 x 256 x 2304 1239 vs 1345 -- twice the barriers per K.)
+//  * A image: row m = 128 K bytes, chunk c at m*128 + 16*(c ^ ((m >> 1) & 7)):
+//    a ds_read_b128 lane group's 16 rows (8 even, 8 odd) on 16 bank quads.
 //  * B image: K rows of 256 N bytes as loaded (no register transpose): chunk b
 //    of row k at k*256 + 16*(b ^ 2(k & 7)).  The MFMA B fragment (16 K bytes
 //    of one column) is two ds_read_b64_tr_b8: per 16-lane group, lane 2q + p
@@ -170,10 +175,6 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_generic_kernel(const int8
 //    x 32 columns on 64 distinct banks.
 //  * The swizzles are applied on the global side: DMA lane t of a piece
 //    fetches the global chunk whose swizzled LDS position is t.
-constexpr int GSLOTS = 4;
-constexpr int GSLOT_A = GT * GK;           // 16 KiB
-constexpr int GSLOT_B = GK * GT;           // 16 KiB
-constexpr int GSLOT_DMA = GSLOT_A + GSLOT_B;
 
 __device__ __attribute__((aligned(64))) int8_t g_zero_gemm[64];
 
@@ -183,36 +184,39 @@ __device__ __forceinline__ v2i ds_tr8(const int8_t* p) {
   return __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)p);
 }
 
-__global__ __launch_bounds__(512, 1) void gemm_s8s8s32_kernel(const int8_t* __restrict__ A,
-                                                             const int8_t* __restrict__ B, int32_t* __restrict__ C,
-                                                             int M, int N, int K, int nbn) {
-  __shared__ __attribute__((aligned(16))) int8_t lds[GSLOTS * GSLOT_DMA];
+constexpr int GK2 = 128;
+constexpr int GSLOT2_A = GT * GK2;  // 32 KiB
+constexpr int GSLOT2 = GSLOT2_A + GK2 * GT;
+
+__global__ __launch_bounds__(512, 1) void gemm_s8s8s32_k128_kernel(const int8_t* __restrict__ A,
+                                                                  const int8_t* __restrict__ B,
+                                                                  int32_t* __restrict__ C, int M, int N, int K,
+                                                                  int nbn) {
+  __shared__ __attribute__((aligned(16))) int8_t lds[2 * GSLOT2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 31, lh = lane >> 5;
   const int l = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (l / nbn) * GT, n0 = (l % nbn) * GT;
   const int wm = wave >> 2, wn = wave & 3;
   const unsigned lds32 = lds_addr32(lds);
-  const int nst = (K + GK - 1) / GK;
+  const int nst = (K + GK2 - 1) / GK2;
 
-  // DMA pieces of a stage: 16 for A (piece j = rows 16j .. 16j+15), 16 for B
-  // (piece j = rows 4j .. 4j+3); wave w issues pieces w, w+8, w+16, w+24.
+  // 64 DMA pieces per stage: 32 for A (piece j = rows 8j .. 8j+7), 32 for B
+  // (piece j = rows 4j .. 4j+3); wave w issues pieces w + 8r, r < 8.
   auto issue = [&](int st) {
-    const int k0 = st * GK;
-    const unsigned slot = lds32 + (st % GSLOTS) * GSLOT_DMA;
+    const int k0 = st * GK2;
+    const unsigned slot = lds32 + (st & 1) * GSLOT2;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 8; ++r) {
       const int pc = wave + 8 * r;
-      const int t = (pc & 15) * 64 + lane;  // chunk index in the image
-      const int8_t* src;
-      if (pc < 16) {
-        const int m = t >> 2, c = (t & 3) ^ ((m >> 2) & 3), k = k0 + 16 * c;
-        src = (m0 + m < M && k < K) ? A + (size_t)(m0 + m) * K + k : g_zero_gemm;
-        glds16_asm(src, slot + (pc & 15) * 1024);
+      if (pc < 32) {
+        const int m = 8 * pc + (lane >> 3), c = (lane & 7) ^ ((m >> 1) & 7), k = k0 + 16 * c;
+        const int8_t* src = (m0 + m < M && k < K) ? A + (size_t)(m0 + m) * K + k : g_zero_gemm;
+        glds16_asm(src, slot + pc * 1024);
       } else {
-        const int k = t >> 4, b = (t & 15) ^ (2 * (k & 7)), n = n0 + 16 * b;
-        src = (k0 + k < K && n < N) ? B + (size_t)(k0 + k) * N + n : g_zero_gemm;
-        glds16_asm(src, slot + GSLOT_A + (pc & 15) * 1024);
+        const int q = pc - 32, k = 4 * q + (lane >> 4), b = (lane & 15) ^ (2 * (k & 7)), n = n0 + 16 * b;
+        const int8_t* src = (k0 + k < K && n < N) ? B + (size_t)(k0 + k) * N + n : g_zero_gemm;
+        glds16_asm(src, slot + GSLOT2_A + q * 1024);
       }
     }
   };
@@ -220,25 +224,22 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_kernel(const int8_t* __re
   v16i acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = v16i{0};
-  for (int st = 0; st < 3 && st < nst; ++st) issue(st);
+  issue(0);
   const int q = (lane & 15) >> 1, p = lane & 1, g = (lane >> 4) & 1;
   for (int s = 0; s < nst; ++s) {
-    const int younger = nst - 1 - s < 2 ? nst - 1 - s : 2;  // stages issued after s (4 pieces each)
-    wait_vm(4 * younger);
+    wait_vm0();  // this wave's pieces of stage s (stage s + 1 is issued below)
     __builtin_amdgcn_s_barrier();
-    // the waitcnt and barrier builtins are not memory operations to the
-    // compiler: this keeps the slot's fragment reads below them
-    asm volatile("" ::: "memory");
-    if (s + 3 < nst) issue(s + 3);  // into the slot stage s - 1 left
-    const int8_t* la = lds + (s % GSLOTS) * GSLOT_DMA;
-    const int8_t* lb = la + GSLOT_A;
+    asm volatile("" ::: "memory");  // the slot's fragment reads stay below the barrier
+    if (s + 1 < nst) issue(s + 1);  // into the slot stage s - 1 left
+    const int8_t* la = lds + (s & 1) * GSLOT2;
+    const int8_t* lb = la + GSLOT2_A;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < 4; ++ks) {
       v4i fa[4], fb[2];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = wm * 128 + i * 32 + lr, c = ks * 2 + lh;
-        fa[i] = *(const v4i*)(la + m * 64 + 16 * (c ^ ((m >> 2) & 3)));
+        fa[i] = *(const v4i*)(la + m * 128 + 16 * (c ^ ((m >> 1) & 7)));
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -273,7 +274,7 @@ hipError_t launch_gemm_s8s8s32(const int8_t* A, const int8_t* B, int32_t* C, int
   const long tiles = (long)nbm * nbn;
   if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
   if (K % 16 == 0 && N % 16 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0) {
-    hipLaunchKernelGGL(gemm_s8s8s32_kernel, dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M, N, K, nbn);
+    hipLaunchKernelGGL(gemm_s8s8s32_k128_kernel, dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M, N, K, nbn);
   } else {
     const int aligned = K % 16 == 0 && N % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 7) == 0;
     hipLaunchKernelGGL(gemm_s8s8s32_generic_kernel, dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M, N, K, nbn,

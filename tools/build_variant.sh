@@ -18,7 +18,8 @@ for f in dlq_amd/csrc/*.hip dlq_amd/csrc/*.cpp; do
   o=$OUT/obj/${b%.*}.o
   objs+=($o)
   if [[ $f == *.cpp ]]; then x="-x hip"; else x=""; fi
-  [ "$b" = block_l1.hip ] && x="$x -fno-slp-vectorize"  # as the Makefile
+  # as the Makefile (block_l1.hip), plus any file named in $NOSLP
+  for n in block_l1.hip $NOSLP; do [ "$b" = $n ] && x="$x -fno-slp-vectorize"; done
   /opt/rocm/bin/hipcc $HIPFLAGS $x -c -o $o $f &
   pids+=($!)
   if [ ${#pids[@]} -ge 8 ]; then wait ${pids[0]}; pids=("${pids[@]:1}"); fi
