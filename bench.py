@@ -274,7 +274,7 @@ def extra_configs(dev):
             tops = 2.0 * M * N * K / (ms * 1e-3) / 1e12
             res[f"{M}x{N}x{K}"] = {"ms": round(ms, 4), "tops": round(tops, 1), "frac": round(tops / PEAK_I8_TOPS, 4)}
             del A, Bm, Cm
-        out["gemm_s8s8s32"] = {"kernel": "gemm_s8s8s32_kernel (gemm.hip)", "peak_tops": round(PEAK_I8_TOPS, 1), **res}
+        out["gemm_s8s8s32"] = {"kernel": "gemm_s8s8s32_k128_kernel (gemm.hip)", "peak_tops": round(PEAK_I8_TOPS, 1), **res}
     except Exception as e:
         out["gemm error"] = repr(e)
     # configs[4]: fp8 (e4m3) activations + per-channel e4m3 weights, B = 256
