@@ -1,6 +1,7 @@
 # Build of the MI355X-native int8 path (hipcc only; no cmake needed).
 #   dlq_amd/libdlq.so  -- the C-ABI library (include/dlq.h)
 #   bin/dlq_e2e        -- the C++ launcher (reference infer_e2e.cu main)
+#   bin/dlq_step       -- the per-step drivers (reference infer_conv1_bn1_relu / infer_layerN / infer_head)
 #   oracle/            -- the CPU checker (test infrastructure; oracle/Makefile)
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
@@ -10,7 +11,7 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -
 SRC = dlq_amd/csrc/kernels.hip dlq_amd/csrc/conv3x3.hip dlq_amd/csrc/conv3x3i.hip dlq_amd/csrc/conv3x3s2i.hip dlq_amd/csrc/block_l1.hip dlq_amd/csrc/stem.hip dlq_amd/csrc/head.hip dlq_amd/csrc/layerops.hip dlq_amd/csrc/gemm.hip dlq_amd/csrc/preproc.hip dlq_amd/csrc/fp8.hip dlq_amd/csrc/ref_f32.hip dlq_amd/csrc/capi.cpp dlq_amd/csrc/resnet18.cpp dlq_amd/csrc/mlp.cpp dlq_amd/csrc/wpack.cpp
 HDR = include/dlq.h dlq_amd/csrc/dlq_internal.h dlq_amd/csrc/device_common.h
 
-all: dlq_amd/libdlq.so bin/dlq_e2e oracle
+all: dlq_amd/libdlq.so bin/dlq_e2e bin/dlq_step oracle
 
 # the layer1 block interleaves its epilogue FMAs with MFMAs: keep them scalar
 build/block_l1.o: HIPFLAGS += -fno-slp-vectorize
@@ -27,6 +28,10 @@ dlq_amd/libdlq.so: build/kernels.o build/conv3x3.o build/conv3x3i.o build/conv3x
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 bin/dlq_e2e: dlq_amd/csrc/main_e2e.cpp dlq_amd/libdlq.so include/dlq.h
+	@mkdir -p bin
+	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -Ldlq_amd -ldlq -Wl,-rpath,'$$ORIGIN/../dlq_amd'
+
+bin/dlq_step: dlq_amd/csrc/main_step.cpp dlq_amd/libdlq.so include/dlq.h
 	@mkdir -p bin
 	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -Ldlq_amd -ldlq -Wl,-rpath,'$$ORIGIN/../dlq_amd'
 

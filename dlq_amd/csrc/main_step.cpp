@@ -1,0 +1,345 @@
+// main_step.cpp -- bin/dlq_step, the per-step C++ drivers of the int8 path.
+//
+// The reference checks its pipeline one stage at a time with standalone
+// drivers that load a stage's weights and a torch fixture, run the stage's
+// kernels, time them and diff the result (CUDA/resnet18-kernel-lab/cpp/fp32/
+// runtime/infer_conv1_bn1_relu.cu:34-156, infer_layer1.cu:130-294,
+// infer_head.cu:16-133: "Diff : max_abs=.. mean_abs=..", exit 0 / 1 usage /
+// 2 fail).  This is their counterpart over the C ABI (include/dlq.h):
+//
+//   dlq_step --step head --manifest DIR --input after_layer4.bin
+//            --expect fc_logits.bin [--expect_prob prob_softmax.bin]
+//     infer_head.cu: the per-layer ABI on the after-layer4 fixture --
+//     dlq_quantize_f32_s8, dlq_gap_s8 (gap_global), dlq_fc_s8 (fc_forward),
+//     dlq_softmax_f32 (softmax_1d) -- each launch timed with hipEvents.
+//
+//   dlq_step --step stem|layer1|layer2|layer3|layer4|gap --manifest DIR
+//            --input image.bin [--expect stage.bin] [--scales FILE]
+//     the stage of the int8 engine's forward on the image (N = 1), against
+//     --expect (a stage fixture or the reference launcher's dump, fp32 NCHW)
+//     or, without it, against the same stage of the reference-semantics fp32
+//     forward on the GPU (dlq_resnet18_forward_f32: the reference's op
+//     sequence, infer_e2e.cu:259-433); the kernel families of the forward are
+//     timed (dlq_resnet18_timing).
+//
+// --out FILE writes the int8 path's result (logits, or the dequantised stage)
+// as fp32 for bit-level checks (tests/test_gpu_step.py).
+//
+// Pass bar: int8 cannot meet the reference's fp32 atol 1e-4, so the bar is
+// relative: max_abs <= --rtol (default 0.1) x max|expected| and, for logits,
+// the same top-1 index.  Both are printed with the diff.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include <unistd.h>
+
+#include "../../include/dlq.h"
+
+#define CHECK_DLQ(x)                                                                                          \
+  do {                                                                                                        \
+    int rc_ = (x);                                                                                            \
+    if (rc_ != DLQ_OK) {                                                                                      \
+      std::fprintf(stderr, "dlq error %d at %s:%d: %s\n", rc_, __FILE__, __LINE__, dlq_last_error());         \
+      return 3;                                                                                               \
+    }                                                                                                         \
+  } while (0)
+#define CHECK_HIP(x)                                                                                          \
+  do {                                                                                                        \
+    hipError_t e_ = (x);                                                                                      \
+    if (e_ != hipSuccess) {                                                                                   \
+      std::fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);                  \
+      return 3;                                                                                               \
+    }                                                                                                         \
+  } while (0)
+
+static void usage() {
+  std::printf(
+      "dlq_step --step head --manifest <dir> --input <after_layer4.bin> --expect <fc_logits.bin>\n"
+      "         [--expect_prob <prob_softmax.bin>] [--rtol R] [--out <logits.bin>]\n"
+      "dlq_step --step stem|layer1|layer2|layer3|layer4|gap --manifest <dir> --input <image.bin>\n"
+      "         [--expect <stage.bin>] [--scales <scales.txt>] [--rtol R] [--out <stage.bin>]\n");
+}
+
+static bool load_f32(const std::string& path, std::vector<float>& v, size_t expect = 0) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  f.seekg(0, std::ios::end);
+  const size_t bytes = (size_t)f.tellg();
+  f.seekg(0);
+  if (bytes % 4 || (expect && bytes != expect * 4)) return false;
+  v.resize(bytes / 4);
+  f.read((char*)v.data(), (std::streamsize)bytes);
+  return (bool)f;
+}
+
+struct Diff {
+  double max_abs = 0, mean_abs = 0, ref_max = 0;
+};
+// diff_max_mean (RK/runtime/utils.hpp) plus the expected tensor's range
+static Diff diff_of(const std::vector<float>& y, const std::vector<float>& e) {
+  Diff d;
+  for (size_t i = 0; i < y.size(); ++i) {
+    const double a = std::fabs((double)y[i] - (double)e[i]);
+    d.max_abs = std::max(d.max_abs, a);
+    d.mean_abs += a;
+    d.ref_max = std::max(d.ref_max, (double)std::fabs(e[i]));
+  }
+  if (!y.empty()) d.mean_abs /= (double)y.size();
+  return d;
+}
+
+static int top1(const std::vector<float>& v) {  // infer_e2e.cu:436-438: first strict maximum
+  int t = -1;
+  float best = -1e30f;
+  for (size_t i = 0; i < v.size(); ++i)
+    if (v[i] > best) best = v[i], t = (int)i;
+  return t;
+}
+
+// ---- infer_head.cu ---------------------------------------------------------
+static void save_f32(const std::string& path, const std::vector<float>& v) {
+  if (path.empty()) return;
+  std::ofstream f(path, std::ios::binary);
+  f.write((const char*)v.data(), (std::streamsize)(v.size() * 4));
+}
+
+static int run_head(const std::string& mani, const std::string& input, const std::string& expect,
+                    const std::string& expect_prob, double rtol, const std::string& out) {
+  std::vector<float> y4, ref_logits, ref_prob, fcw, fcb;
+  if (!load_f32(input, y4) || y4.size() % 512) {
+    std::fprintf(stderr, "open/size fail: %s (want 512 x H x W fp32)\n", input.c_str());
+    return 1;
+  }
+  const int C = 512, HW = (int)(y4.size() / C), K = 1000;
+  if (!load_f32(expect, ref_logits, K) || !load_f32(mani + "/fc.weight.bin", fcw, (size_t)K * C) ||
+      !load_f32(mani + "/fc.bias.bin", fcb, K) || (!expect_prob.empty() && !load_f32(expect_prob, ref_prob, K))) {
+    std::fprintf(stderr, "open/size fail: %s, %s/fc.{weight,bias}.bin or the prob fixture\n", expect.c_str(),
+                 mani.c_str());
+    return 1;
+  }
+  // the feature map's int8 grid: s = max|x| / 127; the GAP keeps it (a mean of
+  // int8 codes is an int8 code), so k = 1 / HW
+  float amax = 0.f;
+  for (float v : y4) amax = std::max(amax, std::fabs(v));
+  const float s = amax > 0.f ? amax / 127.f : 1.f;
+  // fc.weight [1000][512] per-row int8, packed as the 1x1 conv {1, 1, 1, 512 -> 1000}
+  std::vector<int8_t> wq((size_t)K * C);
+  std::vector<float> sw(K);
+  CHECK_DLQ(dlq_quantize_weights_s8(fcw.data(), K, C, wq.data(), sw.data()));
+  const dlq_conv_desc d{1, 1, 1, C, K, 1, 1, 1, 1, 0, 0};
+  std::vector<int8_t> wp(dlq_conv_packed_bytes(&d));
+  CHECK_DLQ(dlq_pack_conv_weights_s8(&d, wq.data(), C, wp.data()));
+  const int ocp = dlq_conv_packed_oc(K);
+  std::vector<float> alpha(ocp, 0.f), bias(ocp, 0.f);
+  for (int o = 0; o < K; ++o) alpha[o] = s * sw[o], bias[o] = fcb[o];
+
+  float *dx, *dal, *dbi, *dlog, *dprob;
+  int8_t *dq, *dg, *dw;
+  CHECK_HIP(hipMalloc(&dx, y4.size() * 4));
+  CHECK_HIP(hipMalloc(&dq, y4.size()));
+  CHECK_HIP(hipMalloc(&dg, C));
+  CHECK_HIP(hipMalloc(&dw, wp.size()));
+  CHECK_HIP(hipMalloc(&dal, ocp * 4));
+  CHECK_HIP(hipMalloc(&dbi, ocp * 4));
+  CHECK_HIP(hipMalloc(&dlog, K * 4));
+  CHECK_HIP(hipMalloc(&dprob, K * 4));
+  CHECK_HIP(hipMemcpy(dx, y4.data(), y4.size() * 4, hipMemcpyHostToDevice));
+  CHECK_HIP(hipMemcpy(dw, wp.data(), wp.size(), hipMemcpyHostToDevice));
+  CHECK_HIP(hipMemcpy(dal, alpha.data(), ocp * 4, hipMemcpyHostToDevice));
+  CHECK_HIP(hipMemcpy(dbi, bias.data(), ocp * 4, hipMemcpyHostToDevice));
+
+  hipEvent_t ev[5];
+  for (auto& e : ev) CHECK_HIP(hipEventCreate(&e));
+  for (int it = 0; it < 2; ++it) {  // the second pass is timed (the first loads the code objects)
+    CHECK_HIP(hipEventRecord(ev[0], nullptr));
+    CHECK_DLQ(dlq_quantize_f32_s8(dx, y4.size(), 1.f / s, dq, nullptr));
+    CHECK_HIP(hipEventRecord(ev[1], nullptr));
+    CHECK_DLQ(dlq_gap_s8(dq, 1, C, HW, 1.f / (float)HW, dg, nullptr));
+    CHECK_HIP(hipEventRecord(ev[2], nullptr));
+    CHECK_DLQ(dlq_fc_s8(dg, 1, C, dw, K, dal, dbi, dlog, nullptr));
+    CHECK_HIP(hipEventRecord(ev[3], nullptr));
+    CHECK_DLQ(dlq_softmax_f32(dlog, 1, K, dprob, nullptr));
+    CHECK_HIP(hipEventRecord(ev[4], nullptr));
+    CHECK_HIP(hipEventSynchronize(ev[4]));
+  }
+  float ms[4];
+  for (int i = 0; i < 4; ++i) CHECK_HIP(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
+
+  std::vector<float> logits(K), prob(K);
+  CHECK_HIP(hipMemcpy(logits.data(), dlog, K * 4, hipMemcpyDeviceToHost));
+  CHECK_HIP(hipMemcpy(prob.data(), dprob, K * 4, hipMemcpyDeviceToHost));
+  save_f32(out, logits);
+  const Diff dl = diff_of(logits, ref_logits);
+  std::printf("Head done (int8: feature scale %.6g, GAP %dx1, FC 1000x512 per-row weights)\n", s, HW);
+  std::printf("  quantize: %.4f ms\n  gap     : %.4f ms\n  fc(gemm): %.4f ms\n  softmax : %.4f ms\n", ms[0], ms[1],
+              ms[2], ms[3]);
+  std::printf("Diff logits : max_abs=%g mean_abs=%g (max|ref|=%g)\n", dl.max_abs, dl.mean_abs, dl.ref_max);
+  bool ok = dl.max_abs <= rtol * dl.ref_max;
+  if (!ref_prob.empty()) {
+    const Diff dp = diff_of(prob, ref_prob);
+    std::printf("Diff prob   : max_abs=%g mean_abs=%g\n", dp.max_abs, dp.mean_abs);
+  }
+  const int t = top1(logits), te = top1(ref_logits);
+  std::printf("top-1       : %d (expected %d)\n", t, te);
+  ok = ok && t == te;
+  for (void* p : {(void*)dx, (void*)dq, (void*)dg, (void*)dw, (void*)dal, (void*)dbi, (void*)dlog, (void*)dprob})
+    (void)hipFree(p);
+  if (ok) {
+    std::printf("[OK] head within the int8 bar (max_abs <= %g x max|ref|, same top-1)\n", rtol);
+    return 0;
+  }
+  std::fprintf(stderr, "[FAIL] head diff exceeded the int8 bar\n");
+  return 2;
+}
+
+// ---- one stage of the engine's forward (infer_conv1_bn1_relu / infer_layerN) ----
+struct StageInfo {
+  const char* step;
+  const char* name;  // dlq_resnet18_stage name
+  const char* site;  // its dequantisation scale's site
+  int C, H;
+};
+static const StageInfo kStages[] = {{"stem", "stem_pool", "conv1", 64, 56},
+                                    {"layer1", "layer1", "layer1.1.conv2", 64, 56},
+                                    {"layer2", "layer2", "layer2.1.conv2", 128, 28},
+                                    {"layer3", "layer3", "layer3.1.conv2", 256, 14},
+                                    {"layer4", "layer4", "layer4.1.conv2", 512, 7},
+                                    {"gap", "gap", "gap", 512, 1}};
+
+static int run_stage(const StageInfo& st, const std::string& mani, const std::string& input, const std::string& expect,
+                     std::string scales, double rtol, const std::string& out) {
+  const size_t img = 3 * 224 * 224, n = (size_t)st.C * st.H * st.H;
+  std::vector<float> x, ref;
+  if (!load_f32(input, x, img)) {
+    std::fprintf(stderr, "open/size fail: %s (want 1x3x224x224 fp32)\n", input.c_str());
+    return 1;
+  }
+  if (!expect.empty() && !load_f32(expect, ref, n)) {
+    std::fprintf(stderr, "open/size fail: %s (want %dx%dx%d fp32)\n", expect.c_str(), st.C, st.H, st.H);
+    return 1;
+  }
+  dlq_resnet18* m = nullptr;
+  CHECK_DLQ(dlq_resnet18_create(&m));
+  CHECK_DLQ(dlq_resnet18_load_manifest(m, mani.c_str()));
+  float *dx, *dlog;
+  CHECK_HIP(hipMalloc(&dx, img * 4));
+  CHECK_HIP(hipMalloc(&dlog, 1000 * 4));
+  CHECK_HIP(hipMemcpy(dx, x.data(), img * 4, hipMemcpyHostToDevice));
+  if (scales.empty()) {
+    std::ifstream f(mani + "/scales.txt");
+    if (f) scales = mani + "/scales.txt";
+  }
+  if (!scales.empty())
+    CHECK_DLQ(dlq_resnet18_load_scales(m, scales.c_str()));
+  else
+    CHECK_DLQ(dlq_resnet18_calibrate(m, dx, 1, 127.0f, nullptr));
+  CHECK_DLQ(dlq_resnet18_set_keep_stages(m, 1));
+  CHECK_DLQ(dlq_resnet18_prepare(m, 1, nullptr));
+  CHECK_DLQ(dlq_resnet18_forward(m, dx, 1, dlog, nullptr));  // untimed: loads the code objects
+  CHECK_DLQ(dlq_resnet18_set_timing(m, 1));
+  CHECK_DLQ(dlq_resnet18_forward(m, dx, 1, dlog, nullptr));
+  double fam_ms[DLQ_FAM_COUNT];
+  int fam_n[DLQ_FAM_COUNT], fwd = 0;
+  CHECK_DLQ(dlq_resnet18_timing(m, fam_ms, fam_n, &fwd));
+  CHECK_DLQ(dlq_resnet18_set_timing(m, 0));
+
+  // the stage, image 0, as fp32 NCHW (int8 NHWC dequantised with its site's scale)
+  std::map<std::string, float> sc;
+  {
+    const std::string tmp = "/tmp/dlq_step_scales_" + std::to_string((long)getpid()) + ".txt";
+    CHECK_DLQ(dlq_resnet18_save_scales(m, tmp.c_str()));
+    std::ifstream f(tmp);
+    std::string line, site;
+    float s;
+    while (std::getline(f, line)) {
+      std::istringstream ss(line);
+      if (!line.empty() && line[0] != '#' && (ss >> site >> s)) sc[site] = s;
+    }
+    std::remove(tmp.c_str());
+  }
+  size_t bytes = 0;
+  CHECK_DLQ(dlq_resnet18_stage(m, st.name, nullptr, 0, &bytes, nullptr));
+  void* tmp = nullptr;
+  CHECK_HIP(hipMalloc(&tmp, bytes));
+  CHECK_DLQ(dlq_resnet18_stage(m, st.name, tmp, bytes, &bytes, nullptr));
+  std::vector<int8_t> q(n);
+  CHECK_HIP(hipMemcpy(q.data(), tmp, n, hipMemcpyDeviceToHost));
+  const float s = sc[st.site];
+  std::vector<float> y(n);
+  for (int h = 0; h < st.H; ++h)
+    for (int w = 0; w < st.H; ++w)
+      for (int c = 0; c < st.C; ++c) y[((size_t)c * st.H + h) * st.H + w] = (float)q[((size_t)h * st.H + w) * st.C + c] * s;
+
+  save_f32(out, y);
+  const char* against = "fixture";
+  if (ref.empty()) {  // the reference-semantics fp32 forward, same stage
+    against = "fp32 reference forward";
+    CHECK_DLQ(dlq_resnet18_forward_f32(m, dx, 1, dlog, nullptr));
+    CHECK_DLQ(dlq_resnet18_stage_f32(m, st.name, nullptr, 0, &bytes, nullptr));
+    void* t32 = nullptr;
+    CHECK_HIP(hipMalloc(&t32, bytes));
+    CHECK_DLQ(dlq_resnet18_stage_f32(m, st.name, t32, bytes, &bytes, nullptr));
+    ref.resize(n);
+    CHECK_HIP(hipMemcpy(ref.data(), t32, n * 4, hipMemcpyDeviceToHost));
+    CHECK_HIP(hipFree(t32));
+  }
+  CHECK_HIP(hipDeviceSynchronize());
+  const Diff d = diff_of(y, ref);
+  static const char* fam_name[DLQ_FAM_COUNT] = {"stem", "layer1 block", "stride-2 + downsample", "wide 3x3",
+                                                "gap+fc", "fc", "other", "fp8 conv"};
+  std::printf("[Step %s] int8 engine, stage %s (%dx%dx%d, scale %.6g) vs %s\n", st.step, st.name, st.C, st.H, st.H, s,
+              against);
+  for (int f = 0; f < DLQ_FAM_COUNT; ++f)
+    if (fam_n[f]) std::printf("  %-22s: %.4f ms (%d launches)\n", fam_name[f], fam_ms[f], fam_n[f]);
+  std::printf("Diff    : max_abs=%g mean_abs=%g (max|ref|=%g, 1 LSB=%g)\n", d.max_abs, d.mean_abs, d.ref_max, s);
+  CHECK_HIP(hipFree(tmp));
+  (void)hipFree(dx);
+  (void)hipFree(dlog);
+  dlq_resnet18_destroy(m);
+  if (d.max_abs <= rtol * d.ref_max) {
+    std::printf("[OK] within the int8 bar (max_abs <= %g x max|ref|)\n", rtol);
+    return 0;
+  }
+  std::fprintf(stderr, "[FAIL] diff exceeded the int8 bar\n");
+  return 2;
+}
+
+int main(int argc, char** argv) {
+  std::string step, mani, input, expect, expect_prob, scales, out;
+  double rtol = 0.1;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    if (a == "--step" && i + 1 < argc) step = argv[++i];
+    else if (a == "--manifest" && i + 1 < argc) mani = argv[++i];
+    else if (a == "--input" && i + 1 < argc) input = argv[++i];
+    else if (a == "--expect" && i + 1 < argc) expect = argv[++i];
+    else if (a == "--expect_prob" && i + 1 < argc) expect_prob = argv[++i];
+    else if (a == "--scales" && i + 1 < argc) scales = argv[++i];
+    else if (a == "--rtol" && i + 1 < argc) rtol = std::atof(argv[++i]);
+    else if (a == "--out" && i + 1 < argc) out = argv[++i];
+  }
+  if (step.empty() || mani.empty() || input.empty()) {
+    usage();
+    return 1;
+  }
+  if (step == "head") {
+    if (expect.empty()) {
+      usage();
+      return 1;
+    }
+    return run_head(mani, input, expect, expect_prob, rtol, out);
+  }
+  for (const auto& st : kStages)
+    if (step == st.step) return run_stage(st, mani, input, expect, scales, rtol, out);
+  usage();
+  return 1;
+}

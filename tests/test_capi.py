@@ -40,6 +40,15 @@ def test_launcher_links_library():
     assert r.returncode == 1 and "--manifest" in r.stdout  # usage, like infer_e2e.cu:221-240
 
 
+def test_step_driver_links_library():
+    exe = os.path.join(ROOT, "bin", "dlq_step")
+    if not os.path.exists(exe):
+        pytest.skip("bin/dlq_step not built")
+    import subprocess
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 1 and "--step head" in r.stdout  # usage, like infer_head.cu:12-14
+
+
 def test_host_quantize_and_fold_match_oracle():
     from dlq_amd import ops
     rng = np.random.default_rng(0)

@@ -14,7 +14,7 @@ pids=()
 objs=()
 for f in dlq_amd/csrc/*.hip dlq_amd/csrc/*.cpp; do
   b=$(basename $f)
-  [ "$b" = main_e2e.cpp ] && continue
+  [ "$b" = main_e2e.cpp ] || [ "$b" = main_step.cpp ] && continue
   o=$OUT/obj/${b%.*}.o
   objs+=($o)
   if [[ $f == *.cpp ]]; then x="-x hip"; else x=""; fi
