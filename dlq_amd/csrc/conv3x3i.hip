@@ -61,7 +61,11 @@ constexpr int ISC = 32;        // input channels per stage
 constexpr int IPITCH = 9 * ISC + 16;  // weight row pitch (304 B, odd multiple of 16: conflict-free)
 constexpr int INW = 8;         // waves per workgroup
 
-template <int W>
+// SPS: 32-channel slices per stage.  The 7x7 launches (C = 512: sixteen
+// one-slice stages of 58.5 MFMAs per SIMD) take two slices per stage, which
+// halves their stage barriers and DMA waits; the 64-oc item's two-slice slot
+// (74 KiB) still fits twice.  The wider items' slots would not.
+template <int W, int SPS = 1>
 struct IGeo {
   static constexpr int H = W;
   static constexpr int RPI = W < 14 ? W : 14;        // output rows per image chunk
@@ -79,16 +83,28 @@ struct IGeo {
   static constexpr int UP = (IPI * CS + 15) / 16 * 16;  // units per 16-channel plane
   static constexpr int PP = (2 * UP + 63) / 64;       // patch DMA pieces (1 KiB)
   static constexpr int ZU = 2 * W + 16;               // zero units read by the edge columns' side taps
-  static constexpr int WB = OT * IPITCH;              // weight bytes per stage
-  static constexpr int WP = WB / 1024;                // weight DMA pieces
-  static constexpr int NPIECE = WP + PP;
-  static constexpr int OFF_Z = WB + PP * 1024;        // zero region, inside each slot (slot-relative addresses)
-  static constexpr int SLOT = OFF_Z + (ZU * 16 + 255) / 256 * 256;
+  static constexpr int WB = OT * IPITCH;              // weight bytes per slice
+  static constexpr int WP = WB / 1024;                // weight DMA pieces per slice
+  static constexpr int ZB = (ZU * 16 + 255) / 256 * 256;
+  // slot (slot-relative addresses): [SPS weight blocks][SPS x (patch, zero region)]
+  static constexpr int WBS = SPS * WB;                // stage weight bytes
+  static constexpr int PB = PP * 1024 + ZB;           // one slice's patch + zero region
+  static constexpr int OFF_P = WBS;                   // slice sub's patch at OFF_P + sub * PB
+  static constexpr int OFF_Z = OFF_P + PP * 1024;     // slice 0's zero region (slice sub: + sub * PB)
+  static constexpr int PPS = SPS * PP, WPS = SPS * WP;  // DMA pieces per stage: patch, weights
+  static constexpr int NPIECE = WPS + PPS;
+  static constexpr int SLOT = WBS + SPS * PB;
   static constexpr int OFF_AB = 2 * SLOT;
-  static_assert(SLOT + 2 * W * 16 + 8 * 32 < 65536, "slot 1 + tap reached by a ds_read immediate offset");
+  // slot bases live in registers (moved per stage); slice and tap offsets are ds_read immediates
+  static_assert((SPS - 1) * PB + 2 * RW * 16 + 16 < 65536 && (SPS - 1) * WB + 8 * 32 < 65536, "immediate offsets");
   static_assert(IPI * RPI * W == IL, "item = whole output rows");
   static_assert(WB % 1024 == 0, "weight block = whole DMA pieces");
 };
+
+template <int W, bool F8>
+constexpr int sps_of() {
+  return W == 7 && !F8 ? 2 : 1;
+}
 
 // Wave -> (oc tile, first px tile, px tile count).  MT = 4: SIMD pair (w, w+4)
 // = oc tile w&3, tiles [0,7) and [7,13).  MT = 2: oc tile w&1, tile groups
@@ -122,13 +138,16 @@ __device__ __forceinline__ void wave_tiles(int wave, int& mt, int& f0, int& nf) 
 // The kernel's LDS constants (zero region, alpha/beta): written after stage
 // 0's DMA is issued so their global-load latency overlaps it; stage 0's
 // barrier publishes them.
-template <int W, int C, int OUT>
+template <int W, int C, int OUT, int SPS>
 __device__ __forceinline__ void conv3x3i_init(const ConvArgs& a, int8_t* lds) {
-  using G = IGeo<W>;
+  using G = IGeo<W, SPS>;
   const int tid = threadIdx.x;
   for (int i = tid; i < G::ZU * 4; i += INW * 64) {
-    ((int*)(lds + G::OFF_Z))[i] = 0;
-    ((int*)(lds + G::SLOT + G::OFF_Z))[i] = 0;
+#pragma unroll
+    for (int sub = 0; sub < SPS; ++sub) {
+      ((int*)(lds + G::OFF_Z + sub * G::PB))[i] = 0;
+      ((int*)(lds + G::SLOT + G::OFF_Z + sub * G::PB))[i] = 0;
+    }
   }
 #ifndef DLQ_X_LATEAB
   if constexpr (OUT == 0) {
@@ -144,11 +163,15 @@ __device__ __forceinline__ void conv3x3i_init(const ConvArgs& a, int8_t* lds) {
 // takes the v_cvt_pk_u8_f32 form (device_common.h quant4_relu).
 template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false, bool RELU = false>
 __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int mt, int f0, int lrank) {
-  using G = IGeo<W>;
-  constexpr int H = W, NS = C / ISC;
+  constexpr int SPS = sps_of<W, F8>();
+  using G = IGeo<W, SPS>;
+  constexpr int H = W, NSL = C / ISC, NS = NSL / SPS;  // 32-channel slices, stages
+  constexpr int KSN = 9 * SPS;                            // k-steps (tap, slice) per stage
   constexpr int OFF_AB = G::OFF_AB;
   constexpr int DPW = (G::NPIECE + NLD - 1) / NLD;  // pieces per loader wave per stage
-  static_assert(DPW <= 18, "at most two DMA pieces per tap");
+  static_assert(DPW <= 2 * KSN, "at most two DMA pieces per k-step");
+  static_assert(!F8 || SPS == 1, "fp8: one slice per stage");
+  static_assert(SPS <= 2, "the piece -> slice selects below");
   const bool loader = lrank >= 0;
   constexpr int STORES = OUT == 0 ? NF : 4 * NF;
   // B fragments two taps ahead for the waves with <= 6 tiles: the younger
@@ -183,9 +206,11 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   // form).  Loader wave lrank issues pieces lrank + NLD k, patch pieces first;
   // every piece's kind is wave-uniform (a scalar branch, no exec masking) and
   // its LDS destination a constant offset in the slot (weights, then patch).
-  constexpr int KP = (G::PP + NLD - 1) / NLD;  // k < KP: possibly a patch piece
+  // With SPS slices per stage, patch piece pc is piece pc % PP of the
+  // stage's slice pc / PP, weight piece wp piece wp % WP of slice wp / WP.
+  constexpr int KP = (G::PPS + NLD - 1) / NLD;  // k < KP: possibly a patch piece
   const int wv = __builtin_amdgcn_readfirstlane(lrank);
-  const int8_t* pptr[KP];  // this wave's patch-piece sources for slice 0 (per item)
+  const int8_t* pptr[KP];  // this wave's patch-piece sources for the item's first stage
   const int8_t* wbase = a.w;  // the issuing item's weight blocks (wave-uniform)
   int iss_li = -1;
   auto prep_issue = [&](int li) {
@@ -193,11 +218,12 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     item_of(li, ot, p0);
     // weight block [ot128][j][128][304]; a 64-oc item is half of one
     const int o128 = (ot * G::OT) >> 7, ohalf = (ot * G::OT) & 127;
-    wbase = a.w + (size_t)(o128 * NS * 128 + ohalf) * IPITCH;
+    wbase = a.w + (size_t)(o128 * NSL * 128 + ohalf) * IPITCH;
     const int R0 = p0 / W;  // first global output row of the item
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
-      const int u = (wv + k * NLD) * 64 + lane;
+      const int pc = wv + k * NLD, sub = SPS > 1 && pc >= G::PP ? 1 : 0;
+      const int u = (pc - sub * G::PP) * 64 + lane;
       const int plane = u >= G::UP ? 1 : 0, q = u - plane * G::UP;
       const int c = q / G::CS, rem = q - c * G::CS;
       const int r = rem / G::RW, iw = rem - r * G::RW;
@@ -206,18 +232,24 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       const bool ok = u < 2 * G::UP && c < G::IPI && r < G::RPI + 2 && n < a.N && (unsigned)ih < (unsigned)H &&
                       (unsigned)iw < (unsigned)W;
       // zero units: a 1 KiB zero block (slice j adds j * 32 and stays inside it)
-      pptr[k] = ok ? a.x + (size_t)(((n * H + ih) * W + iw) * C + plane * 16) : g_zero_i + (lane & 3) * 16;
+      pptr[k] = (ok ? a.x + (size_t)(((n * H + ih) * W + iw) * C + plane * 16) : g_zero_i + (lane & 3) * 16) +
+                sub * ISC;
     }
   };
   auto issue_piece = [&](int s, int k) {  // s < nst
-    const int j = s % NS;
+    const int j0 = (s % NS) * SPS;  // the stage's first slice
     const int pc = wv + k * NLD;
     const unsigned slot = lds32 + (s & 1) * G::SLOT;
-    if (k < KP && pc < G::PP) {
-      glds16_asm(pptr[k < KP ? k : 0] + j * ISC, slot + G::WB + pc * 1024);
-    } else if (pc < G::PP + G::WP) {
-      const int wp = pc - G::PP;
-      glds16_saddr(wbase + (size_t)j * 128 * IPITCH + wp * 1024, (unsigned)lane * 16, slot + wp * 1024);
+    if (k < KP && pc < G::PPS) {
+      const int sub = SPS > 1 && pc >= G::PP ? 1 : 0;
+      glds16_asm(pptr[k < KP ? k : 0] + j0 * ISC, slot + G::OFF_P + sub * G::PB + (pc - sub * G::PP) * 1024);
+    } else if (pc < G::PPS + G::WPS) {
+      const int wp = pc - G::PPS;
+      const int8_t* wsl = wbase + (size_t)j0 * 128 * IPITCH;  // the stage's first slice
+      if (SPS == 1 || wp < G::WP)  // a wave-uniform branch per slice keeps each saddr base scalar
+        glds16_saddr(wsl + wp * 1024, (unsigned)lane * 16, slot + wp * 1024);
+      else
+        glds16_saddr(wsl + 128 * IPITCH + (wp - G::WP) * 1024, (unsigned)lane * 16, slot + wp * 1024);
     }
   };
   auto prep_for = [&](int s) {
@@ -242,7 +274,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     const int c = lp / (G::RPI * W), rem = lp - c * (G::RPI * W);
     const int r = rem / W, ow = rem - r * W;
     const int bu = c * G::CS + r * G::RW + ow;  // tap (kh 0, kw 1): the pixel above
-    const int mid = G::WB + lh * G::UP * 16 + bu * 16;
+    const int mid = G::OFF_P + lh * G::UP * 16 + bu * 16;
     col_off[1][f] = mid;
     col_off[0][f] = ow == 0 ? G::OFF_Z + ((bu - 1) & 15) * 16 : mid - 16;
     col_off[2][f] = ow == W - 1 ? G::OFF_Z + ((bu + 1) & 15) * 16 : mid + 16;
@@ -258,7 +290,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #pragma unroll
     for (int k = 0; k < DPW; ++k) issue_piece(0, k);
   }
-  conv3x3i_init<W, C, OUT>(a, lds);
+  conv3x3i_init<W, C, OUT, SPS>(a, lds);
 
 #ifdef DLQ_X_LATEAB
   // alpha/beta (read only by the epilogue): loaded during stage 0 (their
@@ -363,26 +395,36 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
         }
       }
     } else {
+    // k-step ks = (slice sub = ks / 9, tap = ks % 9) of the stage
+    auto a_at = [&](int ks) -> v4i { return *(const v4i*)(abase + (ks / 9) * G::WB + (ks % 9) * 32); };
+    auto b_off = [&](int ks, int f) {
+      const int tap = ks % 9;
+      return col_off[tap % 3][f] + (tap / 3) * G::RW * 16 + (ks / 9) * G::PB;
+    };
+    auto res_load = [&](int f) {  // the item's residual (store layout), awaited in the epilogue
+      const int p = cur_p0 + (f0 + f) * 32 + lr;
+      const bool keep = (f0 + f) * 32 + lr < IL && p < a.P;
+      const size_t off = keep ? (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16 : 0;
+      rq[f] = gload16_untracked(a.res + off);
+    };
     if constexpr (PF2) {
-    // B fragments two taps ahead: fb[t & 1][f] holds tap t of tile f and is
-    // re-loaded with tap t + 2 right after the MFMA that consumed it (the
-    // LDS latency then has two taps of the SIMD's MFMAs to hide in, enough
+    // B fragments two k-steps ahead: fb[ks & 1][f] holds k-step ks of tile f
+    // and is re-loaded with ks + 2 right after the MFMA that consumed it (the
+    // LDS latency then has two k-steps of the SIMD's MFMAs to hide in, enough
     // for a wave that runs alone at the end of a stage)
     v4i fa[2], fb[2][NF];
-    auto ld_b = [&](int tap, int f) {
-      fb[tap & 1][f] = *(const v4i*)(lds + col_off[tap % 3][f] + (tap / 3) * G::RW * 16);
-    };
-    fa[0] = *(const v4i*)abase;
+    auto ld_b = [&](int ks, int f) { fb[ks & 1][f] = *(const v4i*)(lds + b_off(ks, f)); };
+    fa[0] = a_at(0);
 #pragma unroll
     for (int f = 0; f < NF; ++f) ld_b(0, f);
-    fa[1] = *(const v4i*)(abase + 32);
+    fa[1] = a_at(1);
 #pragma unroll
     for (int f = 0; f < NF; ++f) ld_b(1, f);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int bu = tap & 1;
-      const int k0 = tap * DPW / 9, k1 = (tap + 1) * DPW / 9;
+    for (int ks = 0; ks < KSN; ++ks) {
+      const int bu = ks & 1;
+      const int k0 = ks * DPW / KSN, k1 = (ks + 1) * DPW / KSN;
       if (dma) {
 #pragma unroll
         for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
@@ -390,23 +432,18 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
         acc[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu], fb[bu][f], acc[f], 0, 0, 0);
-        if (f == NF - 1 && tap + 2 < 9) fa[bu] = *(const v4i*)(abase + (tap + 2) * 32);
-        if (tap + 2 < 9) ld_b(tap + 2, f);
+        if (f == NF - 1 && ks + 2 < KSN) fa[bu] = a_at(ks + 2);
+        if (ks + 2 < KSN) ld_b(ks + 2, f);
         if constexpr (OUT == 0 && RES) {
-          if (tap == 8 && j == NS - 1) {
-            const int p = cur_p0 + (f0 + f) * 32 + lr;
-            const bool keep = (f0 + f) * 32 + lr < IL && p < a.P;
-            const size_t off = keep ? (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16 : 0;
-            rq[f] = gload16_untracked(a.res + off);
-          }
+          if (ks == KSN - 1 && j == NS - 1) res_load(f);
         }
       }
-      if (tap + 2 < 9) {
+      if (ks + 2 < KSN) {
 #pragma unroll
         for (int i = 0; i < NF; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
           if (i == NF - 1)
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read (B + the A two taps ahead)
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read (B + the A two k-steps ahead)
           else
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read (B)
           if ((i == 1 && k1 > k0) || (i == 3 && k1 > k0 + 1))
@@ -419,23 +456,21 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       }
     }
     } else {
-    // A double-buffered per tap; each B fragment is re-loaded for the next
-    // tap right after the MFMA that consumed it (one register set per tile).
+    // A double-buffered per k-step; each B fragment is re-loaded for the next
+    // k-step right after the MFMA that consumed it (one register set per tile).
     v4i fa[2], fb[NF];
-    auto ld_b = [&](int tap, int f) {
-      fb[f] = *(const v4i*)(lds + col_off[tap % 3][f] + (tap / 3) * G::RW * 16);
-    };
-    fa[0] = *(const v4i*)abase;
+    auto ld_b = [&](int ks, int f) { fb[f] = *(const v4i*)(lds + b_off(ks, f)); };
+    fa[0] = a_at(0);
 #pragma unroll
     for (int f = 0; f < NF; ++f) ld_b(0, f);
-    // keep tap 0's fragment reads here: left to the scheduler they were sunk
-    // into tap 0's MFMA slots and serialised (one lgkmcnt(0) per MFMA)
+    // keep k-step 0's fragment reads here: left to the scheduler they were sunk
+    // into its MFMA slots and serialised (one lgkmcnt(0) per MFMA)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int bu = tap & 1;
-      if (tap + 1 < 9) fa[bu ^ 1] = *(const v4i*)(abase + (tap + 1) * 32);
-      const int k0 = tap * DPW / 9, k1 = (tap + 1) * DPW / 9;
+    for (int ks = 0; ks < KSN; ++ks) {
+      const int bu = ks & 1;
+      if (ks + 1 < KSN) fa[bu ^ 1] = a_at(ks + 1);
+      const int k0 = ks * DPW / KSN, k1 = (ks + 1) * DPW / KSN;
       if (dma) {
 #pragma unroll
         for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
@@ -443,24 +478,18 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
         acc[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu], fb[f], acc[f], 0, 0, 0);
-        if (tap + 1 < 9) ld_b(tap + 1, f);
+        if (ks + 1 < KSN) ld_b(ks + 1, f);
         if constexpr (OUT == 0 && RES) {
-          // the item's residual (store layout) into the registers this
-          // tile's last B fragment just freed; awaited in the epilogue
-          if (tap == 8 && j == NS - 1) {
-            const int p = cur_p0 + (f0 + f) * 32 + lr;
-            const bool keep = (f0 + f) * 32 + lr < IL && p < a.P;
-            const size_t off = keep ? (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16 : 0;
-            rq[f] = gload16_untracked(a.res + off);
-          }
+          // into the registers this tile's last B fragment just freed
+          if (ks == KSN - 1 && j == NS - 1) res_load(f);
         }
       }
-      if (tap + 1 < 9) {
+      if (ks + 1 < KSN) {
 #pragma unroll
         for (int i = 0; i < NF; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
           if (i == 0)
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read (next tap's A + this tile's B)
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read (next k-step's A + this tile's B)
           else
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
           if ((i == 1 && k1 > k0) || (i == 3 && k1 > k0 + 1))
@@ -562,7 +591,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 
 template <int W, int C, int OUT, bool RES, bool F8 = false, bool RELU = false>
 __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
-  using G = IGeo<W>;
+  using G = IGeo<W, sps_of<W, F8>()>;
   constexpr int OFF_AB = G::OFF_AB;
   constexpr int LDS_TOTAL = OFF_AB + 2 * C * 4;
   static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");

@@ -53,7 +53,7 @@ def need(cond, msg):
 
 
 # ---------------------------------------------------------------- conv3x3i
-def igeo(W):
+def igeo(W, SPS=1):
     IL, ISC, IPITCH = 392, 32, 9 * 32 + 16
     H = W
     RPI = W if W < 14 else 14
@@ -67,27 +67,33 @@ def igeo(W):
     ZU = 2 * W + 16
     WB = OT * IPITCH
     WP = WB // 1024
-    OFF_Z = WB + PP * 1024
-    SLOT = OFF_Z + (ZU * 16 + 255) // 256 * 256
+    ZB = (ZU * 16 + 255) // 256 * 256
+    WBS, PB = SPS * WB, PP * 1024 + ZB   # slot: [SPS weight blocks][SPS x (patch, zero region)]
+    OFF_P = WBS
+    OFF_Z = OFF_P + PP * 1024
+    SLOT = WBS + SPS * PB
     return dict(IL=IL, ISC=ISC, IPITCH=IPITCH, H=H, RPI=RPI, IPI=IPI, OT=OT, MT=OT // 32, RW=RW, CS=CS, UP=UP,
-                PP=PP, ZU=ZU, WB=WB, WP=WP, NPIECE=WP + PP, OFF_Z=OFF_Z, SLOT=SLOT, OFF_AB=2 * SLOT)
+                PP=PP, ZU=ZU, WB=WB, WP=WP, SPS=SPS, WBS=WBS, PB=PB, OFF_P=OFF_P, PPS=SPS * PP, WPS=SPS * WP,
+                NPIECE=SPS * (WP + PP), OFF_Z=OFF_Z, SLOT=SLOT, OFF_AB=2 * SLOT)
 
 
 def check_conv3x3i(W, N):
     C = {28: 128, 14: 256, 7: 512}[W]
-    g = igeo(W)
-    H, IL, OT, NS, NLD = W, g["IL"], g["OT"], C // 32, 8
+    SPS = 2 if W == 7 else 1  # int8: the 7x7 launches take two 32-channel slices per stage (sps_of)
+    g = igeo(W, SPS)
+    H, IL, OT, NSL, NLD = W, g["IL"], g["OT"], C // 32, 8
+    NS = NSL // SPS
     P = N * H * W
     OCp = C
     n_ot, n_pi = OCp // OT, (P + IL - 1) // IL
     NI = n_ot * n_pi
     Gd = min(NI, NCU)
     DPW = (g["NPIECE"] + NLD - 1) // NLD
-    KP = (g["PP"] + NLD - 1) // NLD
+    KP = (g["PPS"] + NLD - 1) // NLD
     lds_total = g["OFF_AB"] + 2 * C * 4
     need(lds_total <= 160 * 1024, "LDS budget")
     xbytes = P * C
-    wbytes = (OCp // 128 if OCp >= 128 else 1) * NS * 128 * g["IPITCH"]
+    wbytes = (OCp // 128 if OCp >= 128 else 1) * NSL * 128 * g["IPITCH"]
     lane = np.arange(64)
     # int32 offset arithmetic of prep_issue: ((n*H+ih)*W+iw)*C + plane*16
     need(P * C < INT_MAX, f"conv3x3i W={W}: N={N} overflows the int pixel offset")
@@ -118,26 +124,32 @@ def check_conv3x3i(W, N):
                  (iw >= 0) & (iw < W)
             src = np.where(ok, ((n * H + ih) * W + iw) * C + plane * 16, -1)
             o128, ohalf = (ot * OT) >> 7, (ot * OT) & 127
-            wbase = (o128 * NS * 128 + ohalf) * g["IPITCH"]
-            for j in range(NS):
+            wbase = (o128 * NSL * 128 + ohalf) * g["IPITCH"]
+            for st in range(NS):
+                j0 = st * SPS  # the stage's first slice
                 issued = np.zeros(g["NPIECE"], int)
                 for wv in range(NLD):
                     for k in range(DPW):
                         pc = wv + k * NLD
-                        if k < KP and pc < g["PP"]:
-                            us = pc * 64 + lane
+                        if k < KP and pc < g["PPS"]:
+                            sub = 1 if (SPS > 1 and pc >= g["PP"]) else 0
+                            p = pc - sub * g["PP"]
+                            j = j0 + sub
+                            us = p * 64 + lane
                             s_ok = src[us] >= 0
                             need(src[us][s_ok] + j * 32 + 16 <= xbytes, "patch source past the input")
                             need(src[us][s_ok] + j * 32 >= 0, "patch source before the input")
                             need((lane[~s_ok] & 3) * 16 + j * 32 + 16 <= 1024, "zero source past the zero block")
-                            dst = g["WB"] + pc * 1024
-                            need(dst + 1024 <= g["OFF_Z"], "patch piece into the zero region")
+                            dst = g["OFF_P"] + sub * g["PB"] + p * 1024
+                            need(dst + 1024 <= g["OFF_Z"] + sub * g["PB"], "patch piece into the zero region")
                             issued[pc] += 1
-                        elif pc < g["PP"] + g["WP"]:
-                            wp = pc - g["PP"]
-                            s0 = wbase + j * 128 * g["IPITCH"] + wp * 1024
+                        elif pc < g["PPS"] + g["WPS"]:
+                            wp = pc - g["PPS"]
+                            sub = 1 if (SPS > 1 and wp >= g["WP"]) else 0
+                            q = wp - sub * g["WP"]
+                            s0 = wbase + (j0 + sub) * 128 * g["IPITCH"] + q * 1024
                             need(s0 >= 0 and s0 + 1024 <= wbytes, "weight piece past the packed image")
-                            need(wp * 1024 + 1024 <= g["WB"], "weight piece past the weight region")
+                            need(sub * g["WB"] + q * 1024 + 1024 <= g["WBS"], "weight piece past the weight region")
                             issued[pc] += 1
                 need(issued == 1, f"conv3x3i W={W}: a piece issued {issued.min()}..{issued.max()} times")
             # tap reads of the item: every output pixel, every tap, both planes
@@ -145,8 +157,9 @@ def check_conv3x3i(W, N):
             valid = (lp_all < IL) & (p < P)
             pn = p // (H * W)
             poh, pow_ = (p % (H * W)) // W, p % W
-            for lh in (0, 1):
-                mid = g["WB"] + lh * g["UP"] * 16 + bu * 16
+            for lh, sub in ((0, 0), (1, 0), (0, SPS - 1), (1, SPS - 1)):
+                mid = g["OFF_P"] + lh * g["UP"] * 16 + bu * 16
+                zo = g["OFF_Z"] + sub * g["PB"]  # this slice's zero region
                 for kh in range(3):
                     for kw in range(3):
                         if kw == 1:
@@ -155,11 +168,12 @@ def check_conv3x3i(W, N):
                             addr = np.where(ow == 0, g["OFF_Z"] + ((bu - 1) & 15) * 16, mid - 16)
                         else:
                             addr = np.where(ow == W - 1, g["OFF_Z"] + ((bu + 1) & 15) * 16, mid + 16)
-                        addr = addr + kh * g["RW"] * 16
+                        addr = addr + kh * g["RW"] * 16 + sub * g["PB"]  # the kernel's b_off
+                        need(addr + 16 <= g["SLOT"], "tap read past the slot")
                         eih, eiw = poh + kh - 1, pow_ + kw - 1
                         inside = (eih >= 0) & (eih < H) & (eiw >= 0) & (eiw < W)
-                        in_zero = (addr >= g["OFF_Z"]) & (addr < g["OFF_Z"] + g["ZU"] * 16)
-                        unit = (addr - g["WB"]) // 16
+                        in_zero = (addr >= zo) & (addr < zo + g["ZU"] * 16)
+                        unit = (addr - g["OFF_P"] - sub * g["PB"]) // 16
                         need((addr % 16 == 0), "unaligned tap read")
                         need(in_zero | ((unit >= 0) & (unit < g["PP"] * 64)), "tap read outside patch and zero region")
                         want = np.where(inside, ((pn * H + eih) * W + eiw) * C + lh * 16, -1)
