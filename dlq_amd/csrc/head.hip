@@ -128,6 +128,59 @@ __global__ __launch_bounds__(64) void linear_kernel(const int8_t* __restrict__ x
   }
 }
 
+// linear_kernel<1> for K = 512 (the ResNet-18 FC on the GAP codes): the same
+// tile, integers and epilogue, but every load -- the 16 k-steps' A and B
+// fragments and the 16 epilogue constants of each kind -- is issued before
+// the first MFMA, so the wave waits for memory once instead of once per
+// four k-steps.  Two independent accumulation chains.
+__global__ __launch_bounds__(64) void linear512_f32_kernel(const int8_t* __restrict__ x, int N,
+                                                           const int8_t* __restrict__ w, int OC, int OCp,
+                                                           const float* __restrict__ alpha,
+                                                           const float* __restrict__ beta, float* __restrict__ y) {
+  constexpr int K = 512, NK = K / 32;
+  const int lane = threadIdx.x, lr = lane & 31, lh = lane >> 5;
+  const int ot = blockIdx.x, rt = blockIdx.y;
+  const int oc = ot * 32 + lr, ol = oc & 63;
+  const int row = min(rt * 32 + lr, N - 1);
+  const int8_t* wp = w + ((size_t)(oc >> 6) * 64 + ol) * 64;
+  const size_t wstride = (size_t)(OCp / 64) * 64 * 64;
+  const int sw = (ol >> 2) & 3;
+  const int8_t* xp = x + (size_t)row * K + lh * 16;
+  v4i a[NK], b[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    a[kk] = *(const v4i*)(wp + (size_t)(kk >> 1) * wstride + ((((2 * kk + lh) & 3) ^ sw) << 4));
+    b[kk] = *(const v4i*)(xp + kk * 32);
+  }
+  float al[16], be[16];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int o = min(ot * 32 + 8 * g + 4 * lh + e, OCp - 1);  // alpha/beta are OCp long
+      al[4 * g + e] = alpha[o];
+      be[4 * g + e] = beta[o];
+    }
+  __builtin_amdgcn_sched_barrier(0);  // every load above is issued before the first MFMA
+  v16i acc0 = v16i{0}, acc1 = v16i{0};
+#pragma unroll
+  for (int kk = 0; kk < NK; kk += 2) {
+    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kk], b[kk], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kk + 1], b[kk + 1], acc1, 0, 0, 0);
+  }
+  const v16i acc = acc0 + acc1;
+  const int r = rt * 32 + lr;
+  if (r >= N) return;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int o0 = ot * 32 + 8 * g + 4 * lh;
+    float* dst = y + (size_t)r * OC + o0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (o0 + e < OC) dst[e] = __builtin_fmaf((float)acc[4 * g + e], al[4 * g + e], be[4 * g + e]);
+  }
+}
+
 // gap_fc_kernel: the network head (GAP + FC, RK/runtime/infer_e2e.cu:417-433)
 // in ONE launch for C = K = 512, fp32 logits -- the same integers and the same
 // float ops as gap16_kernel followed by linear_kernel<1>, so the logits are
@@ -495,7 +548,9 @@ hipError_t launch_linear(const int8_t* x, int N, int K, const int8_t* w, int OC,
                          const float* beta, int relu, int out_kind, void* y, hipStream_t s) {
   const int OCp = packed_oc(OC);
   const dim3 grid((OC + 31) / 32, (N + 31) / 32), block(64);
-  if (out_kind == 1)
+  if (out_kind == 1 && K == 512)
+    hipLaunchKernelGGL(linear512_f32_kernel, grid, block, 0, s, x, N, w, OC, OCp, alpha, beta, (float*)y);
+  else if (out_kind == 1)
     hipLaunchKernelGGL(linear_kernel<1>, grid, block, 0, s, x, N, K, w, OC, OCp, alpha, beta, relu, y);
   else if (out_kind == 2)
     hipLaunchKernelGGL(linear_kernel<2>, grid, block, 0, s, x, N, K, w, OC, OCp, alpha, beta, relu, y);
