@@ -470,7 +470,8 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
         }
       }
     } else {
-      auto epi = [&](const Acc* ac, int ab_off, float lo, int8_t* out, auto rc) {
+      // probe builds: dbg 16 / 32 send the downsample / conv1 stores to the trash line
+      auto epi = [&](const Acc* ac, int ab_off, float lo, int8_t* out, auto rc, bool no_store) {
         constexpr bool RL = decltype(rc)::value;
         float al[4][4], be[4][4];
 #pragma unroll
@@ -503,15 +504,17 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
           swap32(q[0], q[2]);
           swap32(q[1], q[3]);
           const int e = perm_at<OW>((f0 + f) * 32 + lr), p = cur_p0 + (e & 0x3fff);
-          const bool keep = !(e & 0x4000) && p < a.P;
+          const bool keep = !(e & 0x4000) && p < a.P && !no_store;
           v4i* dst = keep ? (v4i*)(out + (size_t)p * a.OC + cur_ot * JOT + mt * 32 + lh * 16)
                           : (v4i*)(g_trash_s2i + lane * 16);
           *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
         }
       };
       constexpr float LO = F8 ? -448.f : -127.f;
-      epi(acc, 0, a.relu ? 0.f : LO, (int8_t*)a.y, std::integral_constant<bool, RELU && !F8>{});
-      if constexpr (DS) epi(accd, 2 * OC * 4, LO, y_ds, std::integral_constant<bool, false>{});
+      epi(acc, 0, a.relu ? 0.f : LO, (int8_t*)a.y, std::integral_constant<bool, RELU && !F8>{}, DLQ_ABL(a, 32));
+      if constexpr (DS) {  // probe builds: dbg 8 skips the downsample's epilogue
+        if (!DLQ_ABL(a, 8)) epi(accd, 2 * OC * 4, LO, y_ds, std::integral_constant<bool, false>{}, DLQ_ABL(a, 16));
+      }
     }
   }
   JSTAMP(62);

@@ -1,6 +1,8 @@
 // Timing probe (not product code): the 196-px stride-2 conv + fused
 // downsample kernel (conv3x3s2i.hip) on the three ResNet-18 shapes, random
-// int8 data, B = 256; argv: OW (28/14/7), dbg bits (2 = no LDS-DMA).
+// int8 data, B = 256; argv: OW (28/14/7), dbg bits (2 = no LDS-DMA, 4 = no
+// epilogues, 8 = no downsample epilogue, 16 / 32 = downsample / conv1 stores
+// to a trash line).
 // With -DDLQ_STAMPS it also prints per-wave s_memtime stamps (prologue,
 // per-stage barrier wait / MFMA loop, epilogues) of three workgroups.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
