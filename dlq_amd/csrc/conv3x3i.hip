@@ -433,7 +433,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       for (int f = 0; f < NF; ++f) {
         acc[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu], fb[bu][f], acc[f], 0, 0, 0);
         if (f == NF - 1 && ks + 2 < KSN) fa[bu] = a_at(ks + 2);
-        if (ks + 2 < KSN) ld_b(ks + 2, f);
+        if (ks + 2 < KSN && !DLQ_ABL(a, 8)) ld_b(ks + 2, f);  // probe builds: dbg 8 re-uses k-steps 0/1's B
         if constexpr (OUT == 0 && RES) {
           if (ks == KSN - 1 && j == NS - 1) res_load(f);
         }
@@ -478,7 +478,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
         acc[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu], fb[f], acc[f], 0, 0, 0);
-        if (ks + 1 < KSN) ld_b(ks + 1, f);
+        if (ks + 1 < KSN && !DLQ_ABL(a, 8)) ld_b(ks + 1, f);  // probe builds: dbg 8 re-uses k-step 0's B
         if constexpr (OUT == 0 && RES) {
           // into the registers this tile's last B fragment just freed
           if (ks == KSN - 1 && j == NS - 1) res_load(f);

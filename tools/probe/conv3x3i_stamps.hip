@@ -1,5 +1,7 @@
 // Timing probe (not product code): per-wave s_memtime stamps of the 392-px
-// wide stride-1 conv kernel (conv3x3i.hip), random int8 data.
+// wide stride-1 conv kernel (conv3x3i.hip), random int8 data; argv: W, dbg
+// bits (2 no LDS-DMA, 4 no epilogue, 8 B fragments read for the first k-steps
+// only), N.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DDLQ_STAMPS \
 //          -I dlq_amd/csrc tools/probe/conv3x3i_stamps.hip -o tools/probe/conv3x3i_stamps
 #define DLQ_ABLATION 1  // the kernel honours a.dbg (timing ablations)
