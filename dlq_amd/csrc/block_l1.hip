@@ -16,7 +16,8 @@
 //   conv2 waves (4-7): output rows [G-9, G-1) from intermediate rows [G-10, G)
 //   all waves:         LDS-DMA of input rows [G+9, G+17) for phase g+1
 // so conv2 trails conv1 by one phase and nothing waits inside a phase; one
-// barrier per phase.
+// barrier per phase.  (block_l1_sp_kernel's last phase gives conv2 nine rows,
+// so the image's last output row needs no phase of its own.)
 //
 // LDS layout: two rings (input, intermediate) of 18 rows + one zero row,
 // each split into four channel planes (plane p = channels 16p .. 16p+15, 16 B
@@ -560,13 +561,17 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
     const int S_in = pos_mod(G - 1, NR), S_mid1 = G % NR, r01 = G % LW;
     const int S_mid2 = pos_mod(G - 10, NR), rr0 = pos_mod(G - 9, LW), jm0 = (G - 9 - rr0) / LW;
     // this phase's jobs k = kb .. ke-1 (tile t = par + 2k; wave-uniform)
+    // The last phase's conv2 takes 9 rows (16 tiles, k < 8): its ninth row
+    // needs intermediate rows up to the image's last, written the phase
+    // before, so no phase is left for that one row.
     int kb = 0, ke = 0;
+    const bool lastp = g == nphase - 1;
     if constexpr (!SECOND) {
       if (G < rows) ke = 7;
-    } else if (G - 9 >= 0 && G - 2 < rows) {  // every output row of the phase exists
+    } else if (!lastp && G - 9 >= 0 && G - 2 < rows) {  // every output row of the phase exists
       ke = 7;
     } else {
-      for (int k = 0; k < 7; ++k) {  // output rows G-9 + (32t .. 32t+31) / 56 must reach [0, rows)
+      for (int k = 0; k < (lastp ? 8 : 7); ++k) {  // output rows G-9 + (32t .. 32t+31) / 56 must reach [0, rows)
         const int t = par + 2 * k;
         const int R0 = G - 9 + (t * 32) / LW, R1 = G - 9 + (t * 32 + 31) / LW;
         const bool any = R1 >= 0 && R0 < rows;
@@ -596,7 +601,7 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
     auto setup = [&](int k, Job& jb) {
       const int t = par + 2 * k;
       const int px = t * 32 + lr;
-      const int ro = (px * 1171) >> 16;  // px / 56 for px < 448
+      const int ro = (px * 1171) >> 16;  // px / 56 for px < 512
       const int col = px - ro * LW;
       if constexpr (!SECOND) {
         int s0 = S_in + ro;
@@ -714,7 +719,7 @@ __global__ __launch_bounds__(512, 1) void block_l1_sp_kernel(BlockArgs a) {
   const int NG = gridDim.x, b = blockIdx.x;
   const int J = (a.N - b + NG - 1) / NG;  // images b, b+NG, ... of this workgroup
   const int rows = J * LW;
-  const int nphase = rows / RPH + 2;  // conv2 trails conv1 by 9 rows
+  const int nphase = rows / RPH + 1;  // conv2 trails conv1 by 9 rows; its last phase takes 9
   for (int i = tid; i < RING / 16; i += 512) *(v4i*)(lds + OFF_MID + 16 * i) = v4i{0, 0, 0, 0};
   for (int i = tid; i < 4 * PROW / 16; i += 512)
     *(v4i*)(lds + OFF_IN + (i >> 6) * PL + NR * PROW + 16 * (i & 63)) = v4i{0, 0, 0, 0};
