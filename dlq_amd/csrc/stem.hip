@@ -365,22 +365,31 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): last step's ring rows and staging
       __builtin_amdgcn_s_barrier();
       ST(0);
-      convert_quad(t + 3, raw[(S + 3) % (PD + 1)]);
-      ST(1);
-      if (t > 0) store_row(p - 1);
-      load_quad(t + 3 + PD, raw[(S + 2) % (PD + 1)]);
-      ST(2);
+      auto ingest = [&]() {
+        convert_quad(t + 3, raw[(S + 3) % (PD + 1)]);
+        ST(1);
+        if (t > 0) store_row(p - 1);
+        load_quad(t + 3 + PD, raw[(S + 2) % (PD + 1)]);
+        ST(2);
+      };
 
       Pv He[8], Ho[8];
 #ifndef DLQ_STEM_SERIAL
       if constexpr (!F8) {
+        // The convert writes conv rows 2p+2 .. 2p+6 and the MFMAs read rows
+        // 2p, 2p+1 (other ring slots), so within a step either may go first:
+        // the MFMAs go first and the convert's VALU runs while they drain
+        // (65.1-65.9 -> 63.7-64.0 us per launch, tools/ab.py, one box,
+        // bit-identical; MFMAs first in waves 4-7 only: 66.8-67.5).
         Acc ce, co;
         conv_rows2(2 * p, ce, co);
+        ingest();
         hpool(ce, He);
         hpool(co, Ho);
       } else
 #endif
       {
+        ingest();
         hpool(conv_row(2 * p), He);
         hpool(conv_row(2 * p + 1), Ho);
       }
