@@ -189,7 +189,18 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
     // of conv rows outside the band land in slots that the band's own rows
     // overwrite before they are read (tools: the stem parity tests at 1..14
     // bands per image).
-    auto convert_quad = [&](int k, const F2 (&r)[3]) {
+    // Scatter addresses (int8): quad k's first conv row is ob0 + 2k (ob0 =
+    // the lane's first conv row of quad 0), so its 4 rows' slots are
+    // (ob0 + j) & 7 with j = (2k + e) & 7 -- static in the unrolled step
+    // loop -- and kh = c0 - 2e with c0 in {6, 7} (the lane's row parity):
+    // one table of 8 slot bases per lane and item, every scatter address an
+    // immediate offset from one of them (per step ~120 -> ~100 VALU; stem
+    // ~64.1 -> ~62.9 us per launch, medians of five A/B rounds on one box).
+    const int ob0 = (iy0 + cv_r - 3) >> 1, kh0 = iy0 + cv_r - 2 * ob0 + 3;
+    int sa[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sa[j] = OFF_CR + ((ob0 + j) & (CR_SLOTS - 1)) * CR_ROW + cv_u * 16 + 2 * kh0 - 12;
+    auto convert_quad = [&](int k, const F2 (&r)[3], auto jc) {  // jc = (2k) & 7
       const int iy = iy0 + 4 * k + cv_r;
       unsigned v[3];
 #pragma unroll
@@ -203,6 +214,17 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
           const unsigned u1 = __float_as_uint(__builtin_amdgcn_fmed3f(r[c][1] * a.inv_s, -127.f, 127.f) + 12582912.0f);
           v[c] = __builtin_amdgcn_perm(u1, u0, 0x0c0c0400u);
         }
+      }
+      if constexpr (!F8) {  // the 4 conv rows' slots from the item's table: immediates only
+        constexpr int J = decltype(jc)::value;
+        static_assert(PD == 3, "jc = (2k) & 7 is static because the step loop is unrolled by 4");
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+            *(unsigned short*)(lds + sa[(J + e) & 7] + (12 - 4 * e + c * CR_PLANE)) = (unsigned short)v[c];
+        }
+        return;
       }
       const int oyb = (iy - 3) >> 1;  // ceil((iy - 4) / 2): the first of the 4 conv rows
 #pragma unroll
@@ -339,11 +361,11 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
     static_assert(PD >= 2, "the prologue converts quads 0..2 from their own sets");
 #pragma unroll
     for (int k = 0; k <= PD; ++k) load_quad(k, raw[k]);
-    convert_quad(0, raw[0]);
+    convert_quad(0, raw[0], std::integral_constant<int, 0>{});
     load_quad(PD + 1, raw[0]);
-    convert_quad(1, raw[1]);
+    convert_quad(1, raw[1], std::integral_constant<int, 2>{});
     load_quad(PD + 2, raw[1]);
-    convert_quad(2, raw[2]);
+    convert_quad(2, raw[2], std::integral_constant<int, 4>{});
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): ring rows written (loads stay in flight)
     __builtin_amdgcn_s_barrier();
     Pv Hp[8];
@@ -373,7 +395,7 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
       __builtin_amdgcn_s_barrier();
       ST(0);
       auto ingest = [&]() {
-        convert_quad(t + 3, raw[(S + 3) % (PD + 1)]);
+        convert_quad(t + 3, raw[(S + 3) % (PD + 1)], std::integral_constant<int, (2 * S + 6) & 7>{});
         ST(1);
         if (t > 0) store_row(p - 1);
         load_quad(t + 3 + PD, raw[(S + 2) % (PD + 1)]);
