@@ -160,9 +160,12 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_generic_kernel(const int8
 
 // ---- aligned operands (K % 16 == 0, N % 16 == 0, 16-byte aligned bases):
 // both tiles stream by LDS-DMA, K = 128 per stage through two slots.  Stage
-// s + 1 is issued right after the barrier that opens stage s (every wave has
-// left stage s - 1's slot by then), so its 64 KB land during stage s's 32
-// MFMAs per wave.  (A 4-slot ring of K = 64 stages, three ahead, measured
+// s + 1 is issued after the barrier that opens stage s (every wave has
+// left stage s - 1's slot by then), one piece after each of k-step 0's 8
+// MFMAs, so its 64 KB land during stage s's 32 MFMAs per wave and the matrix
+// pipe runs while the pieces issue (issued back to back after the barrier:
+// 8192^3 1598-1635 vs 1652-1684 TOPS, 50176 x 256 x 2304 1361-1372 vs
+// 1447-1463, three alternating runs on one box).  (A 4-slot ring of K = 64 stages, three ahead, measured
 // 6-12 % slower on one box: 8192^3 1547 vs 1646 TOPS, 4096^3 1648 vs 1852,
 // 50176 x 256 x 2304 1239 vs 1345 -- twice the barriers per K.)
 //  * A image: row m = 128 K bytes, chunk c at m*128 + 16*(c ^ ((m >> 1) & 7)):
@@ -203,22 +206,29 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_k128_kernel(const int8_t*
 
   // 64 DMA pieces per stage: 32 for A (piece j = rows 8j .. 8j+7), 32 for B
   // (piece j = rows 4j .. 4j+3); wave w issues pieces w + 8r, r < 8.
-  auto issue = [&](int st) {
+  // the zero source once, in SGPRs (re-derived per piece it cost an
+  // s_load + lgkmcnt(0) wait beside the MFMAs)
+  const int8_t* zsrc = g_zero_gemm;
+  asm volatile("" : "+s"(zsrc));
+  auto issue_r = [&](int st, int r) {  // this wave's piece r of stage st
     const int k0 = st * GK2;
     const unsigned slot = lds32 + (st & 1) * GSLOT2;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    {
       const int pc = wave + 8 * r;
       if (pc < 32) {
         const int m = 8 * pc + (lane >> 3), c = (lane & 7) ^ ((m >> 1) & 7), k = k0 + 16 * c;
-        const int8_t* src = (m0 + m < M && k < K) ? A + (size_t)(m0 + m) * K + k : g_zero_gemm;
+        const int8_t* src = (m0 + m < M && k < K) ? A + (size_t)(m0 + m) * K + k : zsrc;
         glds16_asm(src, slot + pc * 1024);
       } else {
         const int q = pc - 32, k = 4 * q + (lane >> 4), b = (lane & 15) ^ (2 * (k & 7)), n = n0 + 16 * b;
-        const int8_t* src = (k0 + k < K && n < N) ? B + (size_t)(k0 + k) * N + n : g_zero_gemm;
+        const int8_t* src = (k0 + k < K && n < N) ? B + (size_t)(k0 + k) * N + n : zsrc;
         glds16_asm(src, slot + GSLOT2_A + q * 1024);
       }
     }
+  };
+  auto issue = [&](int st) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) issue_r(st, r);
   };
 
   v16i acc[4][2];
@@ -230,7 +240,9 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_k128_kernel(const int8_t*
     wait_vm0();  // this wave's pieces of stage s (stage s + 1 is issued below)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // the slot's fragment reads stay below the barrier
+#ifdef DLQ_X_GEMM_OLD
     if (s + 1 < nst) issue(s + 1);  // into the slot stage s - 1 left
+#endif
     const int8_t* la = lds + (s & 1) * GSLOT2;
     const int8_t* lb = la + GSLOT2_A;
 #pragma unroll
@@ -251,9 +263,27 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_k128_kernel(const int8_t*
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+#ifndef DLQ_X_GEMM_OLD
+          // stage s + 1's 8 pieces of this wave (into the slot stage s - 1
+          // left), one after each of k-step 0's MFMAs: the matrix pipe runs
+          // while they issue, instead of idling behind 8 back-to-back DMA
+          // issues after the barrier
+          // (the last stage issues a stage past K: zeros into a slot nobody
+          // reads any more, awaited after the loop)
+          if (ks == 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            issue_r(s + 1, 2 * i + j);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#endif
+        }
     }
   }
+#ifndef DLQ_X_GEMM_OLD
+  wait_vm0();  // the past-K stage's pieces land before the workgroup's LDS is released
+#endif
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
