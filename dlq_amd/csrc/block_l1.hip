@@ -644,7 +644,6 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
         if (k - kb == DLQ_L1_PRIOJ) __builtin_amdgcn_s_setprio(0);
       }
       setup(k, job[A]);
-      if constexpr (!SECOND) dma_some(k - kb < 4 ? 2 : 0);
       v4i bf[3];
       auto ld = [&](auto nc, int buf) {
         constexpr int n = decltype(nc)::value, tap = n >> 1, kh = tap / 3, kw = tap % 3;
@@ -668,6 +667,13 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
         constexpr int young = (s + 2 < KS ? 2 : s + 1 < KS ? 1 : 0);
         asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(bf[s % 3]) : "n"(young) : "memory");
         acc[A] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wr[s], bf[s % 3], acc[A], 0, 0, 0);
+        // conv1 waves: the job's two input-ring pieces (first four jobs of a
+        // phase) issue after the chain's 2nd and 4th MFMAs, beside the matrix
+        // work instead of ahead of it (median of five A/B rounds on one box:
+        // 63.3 -> 62.5 us per launch)
+        if constexpr (!SECOND && (s == 1 || s == 3)) {
+          if (k - kb < 4) dma_some(1);
+        }
       };
       static_for<0, KS>(step);
     };
