@@ -75,6 +75,7 @@ constexpr int LDS_STEM = OFF_WST + 64 * WPITCH_S;  // 66 KiB: two workgroups per
 static_assert(2 * LDS_STEM <= 160 * 1024, "two workgroups per CU");
 constexpr int SK = 192;                  // packed K per output channel
 constexpr int kIntMin = (int)0x80000000;
+typedef int v2i __attribute__((ext_vector_type(2)));
 
 #ifdef DLQ_STAMPS
 // timing-probe builds: per-wave cycle totals by section (no VM ops in the loop)
@@ -380,7 +381,28 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
     // (after its convert), so the LDS round trip and the store issue overlap
     // the next step instead of closing this one.
     const int pxl = lane >> 1, hf = lane & 1;
+    // int8 staging [32 oc][16 px]: lane (oc lr, half lh) writes its 8 pooled
+    // bytes as ONE ds_write_b64 (the 8-byte halves of rows with oc bit 3 set
+    // swapped, so a 16-lane store group covers all 32 banks); the store side
+    // reads it back transposed with two ds_read_b64_tr_b8 (16-lane group g,
+    // lane i = 2r + h: row 8g' + r, px half h; lane i receives px i's 8 oc of
+    // rows 8g' .. 8g' + 7), g' = g then g ^ 1, so the lanes of groups 0 and 2
+    // hold 16 consecutive channels of px i.  Against 8 ds_write_b8 + one
+    // ds_read_b128: ~26 fewer LDS cycles per wave and step (the stem's LDS
+    // traffic -- 18 fragment reads, 12 scatter writes per wave and step --
+    // rivals its MFMA time): 62.9-63.8 -> 61.7-62.0 us per launch, five A/B
+    // rounds on one box, bit-identical.
+    const int tg = lane >> 4, ti = lane & 15;
+    const int8_t* tr1 = stg + (8 * tg + (ti >> 1)) * 16 + 8 * ((ti & 1) ^ (tg & 1));
+    const int8_t* tr2 = stg + (8 * (tg ^ 1) + (ti >> 1)) * 16 + 8 * ((ti & 1) ^ ((tg ^ 1) & 1));
     auto store_row = [&](int p) {
+      if constexpr (!F8) {
+        const v2i r1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)tr1);
+        const v2i r2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)tr2);
+        if ((tg & 1) == 0 && ti < 14)
+          *(v4i*)(a.y + (((size_t)n * 56 + p) * 56 + 14 * q + ti) * 64 + ot * 32 + 8 * tg) = v4i{r1[0], r1[1], r2[0], r2[1]};
+        return;
+      }
       const v4i o = *(const v4i*)(stg + pxl * 32 + hf * 16);
       if (lane < 28) *(v4i*)(a.y + (((size_t)n * 56 + p) * 56 + 14 * q + pxl) * 64 + ot * 32 + hf * 16) = o;
     };
@@ -423,7 +445,20 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
         hpool(conv_row(2 * p + 1), Ho);
       }
       ST(3);
-      // vertical max, epilogue on the pooled values, bytes -> staging [16 px][32 oc]
+      // vertical max, epilogue on the pooled values, bytes -> staging
+      if constexpr (!F8) {  // rne(clamp(y, 0, 127)) as v_cvt_pk_u8_f32(min(y, 127)) (quant4_relu), 8 bytes -> [oc][px]
+        unsigned w[2] = {0u, 0u};
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const Pv v = mx3(Hp[m], He[m], Ho[m]);
+          Hp[m] = Ho[m];
+          const float y = __builtin_fmaf((float)v, al, be);
+          w[m >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(y, 127.f), m & 3, w[m >> 2]);
+        }
+        *(v2i*)(stg + lr * 16 + 8 * (lh ^ ((lr >> 3) & 1))) = v2i{(int)w[0], (int)w[1]};
+        ST(4);
+        return;
+      }
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
         const Pv v = mx3(Hp[m], He[m], Ho[m]);
