@@ -503,6 +503,230 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
   ST_STORE();
 }
 
+// int8 stem, one wave per column quarter computing BOTH channel tiles
+// (stem2_kernel): 4 waves per workgroup, two workgroups per CU (two waves
+// per SIMD, 256 VGPRs each).  Against stem_fused_kernel<false> (8 waves, one
+// channel tile each): the wave keeps all 64 channels' weights in registers
+// (48 VGPRs: no weight fragment reads) and reads each conv row's A fragment
+// once for both tiles -- 12 instead of 36 ds_read_b128 per 24 MFMAs -- and
+// its converter lanes take an input row PAIR (2oy-odd, +1), whose bytes of
+// a conv row are 4 contiguous bytes (kh, kh + 1): one ds_write_b32 per conv
+// row and channel where two lanes issued a ds_write_b16 each.  Same item
+// walk, ring, band logic, pooling and numerics as stem_fused_kernel:
+// 61.5-62.8 -> 59.2-60.6 us per launch (four A/B rounds, one box; -DDLQ_X_STEM1
+// launches the one-tile kernel), bit-identical.
+constexpr int S2W = 4;                          // waves: one per column quarter
+constexpr int STG2 = 64 * 16;                   // per wave: [64 oc][16 px] bytes
+constexpr int OFF_STAGE2 = OFF_CR + CR_SLOTS * CR_ROW;
+constexpr int LDS_STEM2 = OFF_STAGE2 + S2W * STG2;
+static_assert(2 * LDS_STEM2 <= 160 * 1024, "two workgroups per CU");
+
+__global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
+  __shared__ __attribute__((aligned(16))) int8_t lds[LDS_STEM2];
+  const unsigned lds32 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) int8_t*)lds;
+  const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;  // q = column quarter = wave
+  const int lr = lane & 31, lh = lane >> 5;
+  const int nitems = a.N * a.nb;
+
+  // both channel tiles' weight fragments and epilogue constants, in registers
+  v4i wr[2][6];
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+    for (int t = 0; t < 6; ++t) wr[ot][t] = *(const v4i*)(a.w + (ot * 32 + lr) * SK + t * 32 + lh * 16);
+  const float al[2] = {a.alpha[lr], a.alpha[32 + lr]}, be[2] = {a.beta[lr], a.beta[32 + lr]};
+  for (int i = tid; i < CR_SLOTS * CR_ROW / 16; i += S2W * 64) *(v4i*)(lds + OFF_CR + i * 16) = v4i{0, 0, 0, 0};
+  wait_vm_const<0>();
+  __syncthreads();
+  const int pi = ((lr >> 3) << 2) + (lr & 3) + 16 * ((lr >> 2) & 1);
+  const int ox = 28 * q - 1 + pi;
+  const unsigned a_col = lds32 + OFF_CR + (unsigned)(ox + 2 + lh) * 16;
+  int8_t* stg = lds + OFF_STAGE2 + q * STG2;
+
+  // converter lanes: (row pair cv_p of the quad, unit cv_u): a wave = 32 units x 2 pairs
+  const int cv_p = (tid >> 5) & 1, cv_u = (tid & 31) + 32 * (tid >> 6);
+  const bool col_ok = (unsigned)(cv_u - 4) < 112u;
+  // staging read-back (store side): 16-lane group g, lane i; rows 16g + 8(g&1) + r, then 16g + 8(1 - (g&1)) + r
+  const int tg = lane >> 4, ti = lane & 15;
+  const int R1 = 16 * tg + 8 * (tg & 1) + (ti >> 1), R2 = 16 * tg + 8 * (1 - (tg & 1)) + (ti >> 1);
+  const int8_t* tr1 = stg + R1 * 16 + 8 * ((ti & 1) ^ ((R1 >> 3) & 1));
+  const int8_t* tr2 = stg + R2 * 16 + 8 * ((ti & 1) ^ ((R2 >> 3) & 1));
+
+  for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+    const int n = item / a.nb, band = item - n * a.nb;
+    const int py0 = band * a.R, py1 = min(56, py0 + a.R);
+    if (py0 >= py1) continue;
+    const int iy0 = 4 * py0 - 5;  // odd: a pair starts on an odd input row
+    const float* img = a.x + (size_t)n * 3 * 224 * 224;
+    using F2 = float __attribute__((ext_vector_type(2)));
+    F2 raw[PD + 1][2][3];
+    __amdgpu_buffer_rsrc_t rs[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      rs[c] = __builtin_amdgcn_make_buffer_rsrc((void*)(img + (size_t)c * 224 * 224), 0, 224 * 224 * 4, 0x00020000);
+    auto load_quad = [&](int k, F2 (&r)[2][3]) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int iy = iy0 + 4 * k + 2 * cv_p + h, sc = cv_u - 4;
+        const int off = ((unsigned)iy < 224u && col_ok) ? (iy * 224 + 2 * sc) * 4 : 0x40000000;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          r[h][c] = __builtin_bit_cast(F2, __builtin_amdgcn_raw_buffer_load_b64(rs[c], off, 0, 0));
+      }
+    };
+    // pair (iy, iy + 1), iy = iy0 + 4k + 2 cv_p odd: its conv rows are
+    // oyb + e (e < 4), oyb = (iy - 3) / 2 = ob0 + 2k, and in conv row oyb + e
+    // the pair's bytes are 12 - 4e .. 15 - 4e (kh = 6 - 2e, 7 - 2e)
+    const int ob0 = ((iy0 - 3) >> 1) + cv_p;
+    int sa[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sa[j] = OFF_CR + ((ob0 + j) & (CR_SLOTS - 1)) * CR_ROW + cv_u * 16;
+    auto convert_quad = [&](const F2 (&r)[2][3], auto jc) {  // jc = (2k) & 7
+      constexpr int J = decltype(jc)::value;
+      unsigned v[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        unsigned u[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int d = 0; d < 2; ++d)
+            u[2 * h + d] = __float_as_uint(__builtin_amdgcn_fmed3f(r[h][c][d] * a.inv_s, -127.f, 127.f) + 12582912.0f);
+        v[c] = __builtin_amdgcn_perm(u[1], u[0], 0x0c0c0400u) | __builtin_amdgcn_perm(u[3], u[2], 0x04000c0cu);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) *(unsigned*)(lds + sa[(J + e) & 7] + (12 - 4 * e + c * CR_PLANE)) = v[c];
+    };
+    // conv rows oy, oy + 1 x both channel tiles: four chains per k-step on the
+    // A fragments of the two rows (read once) and the resident weights
+    auto conv_rows2 = [&](int oy, v16i (&c)[2][2]) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) c[i][0] = c[i][1] = v16i{0};
+      const unsigned ra0 = a_col + (oy & (CR_SLOTS - 1)) * CR_ROW, ra1 = a_col + ((oy + 1) & (CR_SLOTS - 1)) * CR_ROW;
+      v4i fa0[3], fa1[3];
+#define STEM2_RD(t)                                                                                              \
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa0[(t) % 3]) : "v"(ra0), "n"(((t) >> 1) * CR_PLANE + ((t) & 1) * 32) \
+               : "memory");                                                                                      \
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa1[(t) % 3]) : "v"(ra1), "n"(((t) >> 1) * CR_PLANE + ((t) & 1) * 32) \
+               : "memory")
+#define STEM2_WAIT(t, n) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(fa0[(t) % 3]), "+v"(fa1[(t) % 3]) : "n"(n) : "memory")
+#define STEM2_K(t)                                                                          \
+  c[0][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0[(t) % 3], wr[0][t], c[0][0], 0, 0, 0); \
+  c[0][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0[(t) % 3], wr[1][t], c[0][1], 0, 0, 0); \
+  c[1][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1[(t) % 3], wr[0][t], c[1][0], 0, 0, 0); \
+  c[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1[(t) % 3], wr[1][t], c[1][1], 0, 0, 0)
+      STEM2_RD(0);
+      STEM2_RD(1);
+      STEM2_WAIT(0, 2);
+      STEM2_K(0);
+      STEM2_RD(2);
+      STEM2_WAIT(1, 2);
+      STEM2_K(1);
+      STEM2_RD(3);
+      STEM2_WAIT(2, 2);
+      STEM2_K(2);
+      STEM2_RD(4);
+      STEM2_WAIT(3, 2);
+      STEM2_K(3);
+      STEM2_RD(5);
+      STEM2_WAIT(4, 2);
+      STEM2_K(4);
+      STEM2_WAIT(5, 0);
+      STEM2_K(5);
+#undef STEM2_RD
+#undef STEM2_WAIT
+#undef STEM2_K
+    };
+    auto hpool = [&](const v16i& c, int (&H)[8]) {
+      unsigned x0 = (unsigned)c[0], c16 = x0;
+      swap32(x0, c16);
+      const int c0v = (q == 0 && lh == 0) ? kIntMin : c[0];
+      H[0] = max3i(c0v, c[1], c[2]);
+#pragma unroll
+      for (int m = 1; m < 7; ++m) H[m] = max3i(c[2 * m], c[2 * m + 1], c[2 * m + 2]);
+      H[7] = max3i(c[14], c[15], (int)c16);
+    };
+
+    // prologue as stem_fused_kernel: quads 0..2 converted, 3 .. 2+PD loaded
+#pragma unroll
+    for (int k = 0; k <= PD; ++k) load_quad(k, raw[k]);
+    convert_quad(raw[0], std::integral_constant<int, 0>{});
+    load_quad(PD + 1, raw[0]);
+    convert_quad(raw[1], std::integral_constant<int, 2>{});
+    load_quad(PD + 2, raw[1]);
+    convert_quad(raw[2], std::integral_constant<int, 4>{});
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+    int Hp[2][8];
+    if (py0 == 0) {
+#pragma unroll
+      for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+        for (int m = 0; m < 8; ++m) Hp[ot][m] = kIntMin;
+    } else {
+      // conv row 2py0 - 1 (its pair partner 2py0 is computed and discarded)
+      v16i c[2][2];
+      conv_rows2(2 * py0 - 1, c);
+      hpool(c[0][0], Hp[0]);
+      hpool(c[0][1], Hp[1]);
+    }
+    auto store_row = [&](int p) {
+      const v2i r1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)tr1);
+      const v2i r2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)tr2);
+      const v4i o = (tg & 1) ? v4i{r2[0], r2[1], r1[0], r1[1]} : v4i{r1[0], r1[1], r2[0], r2[1]};
+      if (ti < 14) *(v4i*)(a.y + (((size_t)n * 56 + p) * 56 + 14 * q + ti) * 64 + 16 * tg) = o;
+    };
+    auto step = [&](int t, auto setc) {
+      constexpr int S = decltype(setc)::value;
+      const int p = py0 + t;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_s_barrier();
+      v16i c[2][2];
+      conv_rows2(2 * p, c);
+      convert_quad(raw[(S + 3) % (PD + 1)], std::integral_constant<int, (2 * S + 6) & 7>{});
+      if (t > 0) store_row(p - 1);
+      load_quad(t + 3 + PD, raw[(S + 2) % (PD + 1)]);
+#pragma unroll
+      for (int ot = 0; ot < 2; ++ot) {
+        int He[8], Ho[8];
+        hpool(c[0][ot], He);
+        hpool(c[1][ot], Ho);
+        unsigned w[2] = {0u, 0u};
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const int v = max3i(Hp[ot][m], He[m], Ho[m]);
+          Hp[ot][m] = Ho[m];
+          const float y = __builtin_fmaf((float)v, al[ot], be[ot]);
+          w[m >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(y, 127.f), m & 3, w[m >> 2]);
+        }
+        const int row = ot * 32 + lr;
+        *(v2i*)(stg + row * 16 + 8 * (lh ^ ((row >> 3) & 1))) = v2i{(int)w[0], (int)w[1]};
+      }
+    };
+    const int nsteps = py1 - py0;
+    static_assert(PD == 3, "the step loop below is unrolled by 4");
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    int t = 0;
+    for (; t + 4 <= nsteps; t += 4) {
+      step(t, I0{});
+      step(t + 1, I1{});
+      step(t + 2, I2{});
+      step(t + 3, I3{});
+    }
+    if (t < nsteps) step(t, I0{});
+    if (t + 1 < nsteps) step(t + 1, I1{});
+    if (t + 2 < nsteps) step(t + 2, I2{});
+    if (py1 > py0) store_row(py1 - 1);
+    wait_vm0();
+    __syncthreads();
+  }
+}
+
 int num_cus_stem() {
   static int n = 0;
   if (!n) {
@@ -562,7 +786,11 @@ hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float
   if (f8)
     hipLaunchKernelGGL(stem_fused_kernel<true>, dim3(grid), dim3(SNW * 64), 0, s, a);
   else
+#ifdef DLQ_X_STEM1
     hipLaunchKernelGGL(stem_fused_kernel<false>, dim3(grid), dim3(SNW * 64), 0, s, a);
+#else
+    hipLaunchKernelGGL(stem2_kernel, dim3(grid), dim3(S2W * 64), 0, s, a);
+#endif
   return hipGetLastError();
 }
 
