@@ -31,7 +31,7 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from dlq_amd.lib import FAMILIES  # noqa: E402  (pure-Python constant; loads no library)
 
-PREFIX = [("stem_fused_kernel", 0), ("block_l1_kernel", 1), ("block_l1_sp_kernel", 1), ("conv3x3s1_kernel", 1), ("conv3x3s2i_kernel", 2),
+PREFIX = [("stem_fused_kernel", 0), ("stem2_kernel", 0), ("block_l1_kernel", 1), ("block_l1_sp_kernel", 1), ("conv3x3s1_kernel", 1), ("conv3x3s2i_kernel", 2),
           ("conv3x3s2_kernel", 2), ("conv3x3i_kernel", 3), ("conv3x3w_kernel", 3), ("gap16_kernel", 4), ("gap_fc_kernel", 4),
           ("linear_kernel", 5)]
 
