@@ -553,7 +553,7 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
   // the SIMD's issue arbitration against their conv1 partner, which then
   // spends less of the phase waiting at the barrier
 #ifndef DLQ_L1_PRIOJ
-#define DLQ_L1_PRIOJ 5  // measured: 5 of 7 jobs 64.2-64.5 us, all 7 66.0, none 65.9-67.4 (tools/probe/block_l1_sp_stamps.hip)
+#define DLQ_L1_PRIOJ 6  // measured: 5 of 7 jobs 64.2-64.5 us, all 7 66.0, none 65.9-67.4 (tools/probe/block_l1_sp_stamps.hip); with the DMA inside the conv1 chains 6 of 7: median 61.4 vs 62.3 (5) and 62.0 (4) us, four A/B rounds
 #endif
   BT_DECL;
   for (int g = 0; g < nphase; ++g) {
