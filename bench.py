@@ -5,8 +5,14 @@ One step = one forward of the int8 ResNet-18 over the per-rank batch
 (default 256 images, BASELINE.json configs[2]) through libdlq.so, inputs
 already resident in HBM, followed (N > 1) by the RCCL all-gather of the fp32
 logits over xGMI (configs[3]: batch 256*N sharded across N GPUs).
-Launch:  python bench.py [--gpus 1 --steps K --warmup W]
+Launch:  python bench.py [--gpus N --steps K --warmup W]
          python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N
+rank processes itself (before this process touches the GPU) and exits with
+their status; under torch.distributed.run, --gpus must equal WORLD_SIZE.
+Rank r drives GPU LOCAL_RANK % device_count; the exchange is RCCL ("nccl") on
+device tensors when every rank has a GPU of its own, else gloo through host
+copies (DLQ_DIST_BACKEND overrides; the JSON line names the transport).
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
 from __future__ import annotations
@@ -15,6 +21,9 @@ import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
+import sys
 import time
 
 import numpy as np
@@ -47,16 +56,70 @@ def parse():
     return ap.parse_args()
 
 
-def setup_dist():
+def spawn_ranks(n):
+    """--gpus N > 1 without a launcher: start N copies of this script as ranks
+    0..N-1 of one job (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as
+    torch.distributed.run sets them) and return the first non-zero exit
+    status, or 0.  The caller has not touched the GPU (each rank is a fresh
+    process; nothing is exec'd in place).  If one rank fails, the others are
+    terminated by PID so the job cannot hang on a missing peer."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(0.05)
+    return rc
+
+
+def dist_backend(world, ndev):
+    """RCCL ("nccl") when every rank has a GPU of its own, else gloo (ranks
+    sharing a GPU gather through host tensors); DLQ_DIST_BACKEND overrides."""
+    forced = os.environ.get("DLQ_DIST_BACKEND")
+    if forced:
+        if forced not in ("nccl", "gloo"):
+            raise SystemExit(f"bench.py: DLQ_DIST_BACKEND={forced!r} (want nccl or gloo)")
+        return forced
+    return "nccl" if world <= ndev else "gloo"
+
+
+def setup_dist(gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+                         f"(--nproc-per-node {gpus}) or drop the launcher and let --gpus spawn the ranks")
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    dev_index = local % ndev
+    torch.cuda.set_device(dev_index)
+    backend = None
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    return rank, world, local
+        backend = dist_backend(world, ndev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
+    return rank, world, dev_index, backend
 
 
 def shard_gather(forward, x_local, world, out_global=None):
@@ -257,6 +320,8 @@ def extra_configs(dev):
             "us_per_forward_python_loop": round(host_ms * 1e3, 2),
             "timing": "graph of 50 back-to-back forwards replayed 20x (device time per forward); "
                       "python_loop = one ctypes call per forward",
+            "method": "value / us_per_forward are graph-replay device time since round 3; rounds 1-2 "
+                      "reported the python loop, kept here as us_per_forward_python_loop",
             "note": "0.21 GOP per forward in ONE launch (mlp_fused_kernel): latency bound, not MFMA bound"}
     except Exception as e:
         out["configs[1] error"] = repr(e)
@@ -300,7 +365,7 @@ def extra_configs(dev):
 
 def main():
     args = parse()
-    rank, world, local = setup_dist()
+    rank, world, local, backend = setup_dist(args.gpus)
     dev = torch.device("cuda", local)
     from dlq_amd.lib import FAMILIES
     from dlq_amd.models import ResNet18Int8, resnet18_state_dict
@@ -322,8 +387,20 @@ def main():
     std = torch.tensor([0.229, 0.224, 0.225], device=dev).view(1, 3, 1, 1)
     x = ((pix.float() / 255.0 - mean) / std).contiguous()
     del pix
-    pipe = GatherPipeline(lambda xx, out: model.forward(xx, out), B, world, dev)
-    logits = pipe.logits[0]
+    if backend == "gloo":
+        # ranks sharing a GPU: the gather runs through host tensors (gloo has
+        # no device all-gather); the D2H copy of the logits is inside the step
+        dev_logits = torch.empty((B, 1000), dtype=torch.float32, device=dev)
+
+        def fwd_into(xx, out):
+            model.forward(xx, dev_logits)
+            out.copy_(dev_logits.cpu())
+
+        pipe = GatherPipeline(fwd_into, B, world, "cpu")
+        logits = dev_logits
+    else:
+        pipe = GatherPipeline(lambda xx, out: model.forward(xx, out), B, world, dev)
+        logits = pipe.logits[0]
     fwd = lambda xx: model.forward(xx, logits)  # noqa: E731
 
     for _ in range(args.warmup):
@@ -350,7 +427,7 @@ def main():
     model.set_timing(False)
     fam_macs, fam_bytes = model.family_work()
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -409,7 +486,10 @@ def main():
                 f"CPU-calibrated {args.precision} scales)",
         "config": {"workload": workload,
                    "global_batch": world * B, "per_gpu_batch": B,
-                   "parallelism": f"dp{world}" if world > 1 else "single"},
+                   "parallelism": f"dp{world}" if world > 1 else "single",
+                   "exchange": ("none" if world == 1 else
+                                "RCCL all_gather_into_tensor of fp32 logits (device tensors)" if backend == "nccl" else
+                                "gloo all_gather of fp32 logits through host tensors (ranks share a GPU)")},
         "roofline": {"bound": "mfma", "kernel": FAMILIES[dom],
                      "achieved": round(achieved, 1), "peak": round(PEAK_I8_TOPS, 1),
                      "unit": "TFLOP/s", "int8_ops": not fp8,
@@ -443,4 +523,7 @@ def main():
 
 
 if __name__ == "__main__":
+    _args = parse()
+    if _args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(_args.gpus))
     main()

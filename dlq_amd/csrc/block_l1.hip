@@ -705,6 +705,9 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
       }
     }
     BT(1);
+    // a phase of fewer than DLQ_L1_PRIOJ jobs never reached the lowering
+    // above: every phase starts from priority 0
+    if constexpr (SECOND) __builtin_amdgcn_s_setprio(0);
     if constexpr (!SECOND) {
       dma_some(8);
       wait_vm0();  // this phase's DMA has landed
@@ -756,8 +759,8 @@ hipError_t launch_block_l1(const int8_t* x, int N, const int8_t* w1, const float
   if (N <= 0) return hipSuccess;
   BlockArgs a{x, y, w1, w2, a1, b1, a2, b2, s_res, N};
   int grid = num_cus_b();
-  if (const char* e = std::getenv("DLQ_L1_GRID")) {  // test knob: several images per workgroup
-    const int g = std::atoi(e);
+  {  // knob "l1_grid" (DLQ_L1_GRID, dlq_set_knob): several images per workgroup
+    const int g = g_knob_l1_grid.load(std::memory_order_relaxed);
     if (g > 0 && g < grid) grid = g;
   }
   if (f8)

@@ -113,11 +113,46 @@ void pack_conv_weights_for(int C, int OC, int H, int W, int kH, int kW, int sH, 
     pack_conv_weights(q, OC, IC, kH, kW, C, out);
 }
 
+namespace {
+int env_int(const char* name) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : 0;
+}
+}  // namespace
+
+std::atomic<int> g_knob_l1_grid{env_int("DLQ_L1_GRID")};
+std::atomic<int> g_knob_head_split{env_int("DLQ_HEAD_SPLIT")};
+std::atomic<int> g_knob_graph{env_int("DLQ_GRAPH")};
+
+namespace {
+std::atomic<int>* knob(const char* name) {
+  if (!name) return nullptr;
+  if (!std::strcmp(name, "l1_grid")) return &g_knob_l1_grid;
+  if (!std::strcmp(name, "head_split")) return &g_knob_head_split;
+  if (!std::strcmp(name, "graph")) return &g_knob_graph;
+  return nullptr;
+}
+}  // namespace
+
 }  // namespace dlq
 
 using namespace dlq;
 
 extern "C" {
+
+int dlq_set_knob(const char* name, int value) {
+  std::atomic<int>* k = knob(name);
+  if (!k) return fail(DLQ_ERR_ARG, "set_knob: unknown knob");
+  k->store(value);
+  return DLQ_OK;
+}
+
+int dlq_get_knob(const char* name, int* value) {
+  std::atomic<int>* k = knob(name);
+  if (!k || !value) return fail(DLQ_ERR_ARG, "get_knob: unknown knob or null value");
+  *value = k->load();
+  return DLQ_OK;
+}
 
 const char* dlq_version(void) { return "dlq-mi355x 0.1.0 (gfx950, int8 MFMA)"; }
 const char* dlq_last_error(void) { return g_err.c_str(); }

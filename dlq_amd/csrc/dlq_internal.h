@@ -1,12 +1,18 @@
 // dlq_internal.h -- shared declarations between the HIP kernels (kernels.hip)
 // and the host side (capi.cpp, resnet18.cpp, mlp.cpp).  Not installed.
 #pragma once
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <string>
 
 namespace dlq {
+
+// Host-side knobs behind dlq_set_knob (capi.cpp): initialised once from the
+// environment when the library loads, never read from it on the hot path.
+extern std::atomic<int> g_knob_l1_grid, g_knob_head_split, g_knob_graph;
+
 
 // Conv launch parameters (device view).  Activations are NHWC int8.
 struct ConvArgs {
@@ -90,6 +96,9 @@ hipError_t launch_linear(const int8_t* x, int N, int K, const int8_t* w, int OC,
 hipError_t launch_mlp_fused(const float* x, int N, int in, int kp, float inv_s, const int8_t* w1, int H,
                             const float* a1, const float* b1, const int8_t* w2, int OC, const float* a2,
                             const float* b2, int8_t* hq, float* y, hipStream_t s, int mr = 0);
+// false: the fused kernel's LDS (rows, hidden layer, alpha/beta) exceeds 64 KiB
+// for this shape; dlq_mlp_forward then runs quantize_rows + two linear launches.
+bool mlp_fused_fits(int kp, int H, int OC, int mr = 0);
 hipError_t launch_gap_fc(const int8_t* x, int N, int C, int HW, float k, const int8_t* w, int OC,
                          const float* alpha, const float* beta, float* y, hipStream_t s);  // C == 512, HW <= 56
 // dlq_gemm_s8s8s32 (gemm.hip): row-major int8 A[M][K] . B[K][N] -> int32 C.

@@ -505,10 +505,24 @@ __global__ __launch_bounds__(MLP_NW * 64) void mlp_fused_kernel(
 
 // The fused MNIST forward: kp % 64 == 0, kp >= in, H % 64 == 0.
 template <int MR>
+size_t mlp_lds_bytes(int kp, int H, int OC) {
+  return (size_t)MR * (kp + 16) + (size_t)MR * (H + 16) + (size_t)(2 * H + 2 * packed_oc(OC)) * 4;
+}
+
+// The fused kernel's dynamic LDS must fit the 64 KiB it is launched with.
+bool mlp_fused_fits(int kp, int H, int OC, int mr) {
+  if (mr == 0) mr = MLP_MR_DEFAULT;
+  const size_t lds = mr == 16 ? mlp_lds_bytes<16>(kp, H, OC)
+                     : mr == 8 ? mlp_lds_bytes<8>(kp, H, OC)
+                               : mlp_lds_bytes<4>(kp, H, OC);
+  return lds <= 64 * 1024;
+}
+
+template <int MR>
 hipError_t launch_mlp_mr(const float* x, int N, int in, int kp, float inv_s, const int8_t* w1, int H,
                          const float* a1, const float* b1, const int8_t* w2, int OC, const float* a2,
                          const float* b2, int8_t* hq, float* y, hipStream_t s) {
-  const size_t lds = (size_t)MR * (kp + 16) + (size_t)MR * (H + 16) + (size_t)(2 * H + 2 * packed_oc(OC)) * 4;
+  const size_t lds = mlp_lds_bytes<MR>(kp, H, OC);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(mlp_fused_kernel<MR>, dim3((N + MR - 1) / MR), dim3(MLP_NW * 64), lds, s, x, N, in, kp, inv_s,
                      w1, H, packed_oc(H), a1, b1, w2, OC, packed_oc(OC), a2, b2, hq, y);

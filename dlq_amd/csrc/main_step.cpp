@@ -273,7 +273,12 @@ static int run_stage(const StageInfo& st, const std::string& mani, const std::st
   CHECK_DLQ(dlq_resnet18_stage(m, st.name, tmp, bytes, &bytes, nullptr));
   std::vector<int8_t> q(n);
   CHECK_HIP(hipMemcpy(q.data(), tmp, n, hipMemcpyDeviceToHost));
-  const float s = sc[st.site];
+  const auto site = sc.find(st.site);
+  if (site == sc.end()) {
+    std::fprintf(stderr, "[Step %s] no activation scale for site %s in the saved scales\n", st.step, st.site);
+    return 3;
+  }
+  const float s = site->second;
   std::vector<float> y(n);
   for (int h = 0; h < st.H; ++h)
     for (int w = 0; w < st.H; ++w)

@@ -8,7 +8,10 @@
 // The whole forward is ONE launch (head.hip mlp_fused_kernel: quantise, fc1 +
 // bias + ReLU + requant, fc2 + bias, the hidden layer kept in LDS); the
 // reference issues five kernels and a cudaDeviceSynchronize per op
-// (v4.cu:260-265).
+// (v4.cu:260-265).  Shapes whose rows + hidden layer do not fit the fused
+// kernel's 64 KiB of LDS (wide inputs or hidden layers, e.g. in 16K or
+// hidden 8192) run the same integer sums and IEEE epilogues as three
+// launches: quantize_rows -> linear (+ ReLU, requant) -> linear (fp32 out).
 #include <cstring>
 #include <vector>
 
@@ -23,7 +26,8 @@ struct dlq_mlp {
   int8_t* w1 = nullptr;  // packed [OCp(hidden)][kp]
   int8_t* w2 = nullptr;  // packed [OCp(out)][hidden]
   float *a1 = nullptr, *b1 = nullptr, *a2 = nullptr, *b2 = nullptr;
-  int8_t* xq = nullptr;  // [max_batch][kp]
+  bool fused = true;      // mlp_fused_fits(kp, hidden, out)
+  int8_t* xq = nullptr;  // [max_batch][kp], the three-launch path only
   int8_t* hq = nullptr;  // [max_batch][hidden]
   std::vector<void*> allocs;
 };
@@ -85,10 +89,11 @@ int dlq_mlp_create(int in, int hidden, int out, const float* W1, const float* b1
   auto* m = new dlq_mlp();
   m->in = in; m->hidden = hidden; m->out = out; m->kp = (in + 63) / 64 * 64;
   m->max_batch = max_batch; m->s_in = s_in; m->s_hidden = s_hidden;
+  m->fused = mlp_fused_fits(m->kp, hidden, out);
   int rc;
   if ((rc = prep_layer(m, W1, b1, in, hidden, m->kp, s_in, s_hidden, &m->w1, &m->a1, &m->b1)) ||
       (rc = prep_layer(m, W2, b2, hidden, out, hidden, s_hidden, 0.f, &m->w2, &m->a2, &m->b2)) ||
-      (rc = up(m, (void**)&m->xq, nullptr, (size_t)max_batch * m->kp)) ||
+      (!m->fused && (rc = up(m, (void**)&m->xq, nullptr, (size_t)max_batch * m->kp))) ||
       (rc = up(m, (void**)&m->hq, nullptr, (size_t)max_batch * hidden))) {
     dlq_mlp_destroy(m);
     return rc;
@@ -108,9 +113,16 @@ int dlq_mlp_forward(dlq_mlp* m, const float* x, int B, float* logits, void* stre
   if (B < 0 || B > m->max_batch) return fail(DLQ_ERR_ARG, "mlp_forward: batch exceeds max_batch");
   if (B == 0) return DLQ_OK;
   if (!x || !logits) return fail(DLQ_ERR_ARG, "mlp_forward: null argument");
-  const hipError_t e = launch_mlp_fused(x, B, m->in, m->kp, 1.0f / m->s_in, m->w1, m->hidden, m->a1, m->b1, m->w2,
-                                        m->out, m->a2, m->b2, m->hq, logits, (hipStream_t)stream);
-  return e == hipSuccess ? DLQ_OK : hip_fail(e, "mlp_forward");
+  const hipStream_t s = (hipStream_t)stream;
+  if (m->fused) {
+    const hipError_t e = launch_mlp_fused(x, B, m->in, m->kp, 1.0f / m->s_in, m->w1, m->hidden, m->a1, m->b1, m->w2,
+                                          m->out, m->a2, m->b2, m->hq, logits, s);
+    return e == hipSuccess ? DLQ_OK : hip_fail(e, "mlp_forward");
+  }
+  hipError_t e = launch_quantize_rows(x, B, m->in, m->kp, 1.0f / m->s_in, m->xq, s);
+  if (e == hipSuccess) e = launch_linear(m->xq, B, m->kp, m->w1, m->hidden, m->a1, m->b1, 1, 0, m->hq, s);
+  if (e == hipSuccess) e = launch_linear(m->hq, B, m->hidden, m->w2, m->out, m->a2, m->b2, 0, 1, logits, s);
+  return e == hipSuccess ? DLQ_OK : hip_fail(e, "mlp_forward (three-launch path)");
 }
 
 int dlq_mlp_copy_hidden(const dlq_mlp* m, int B, int8_t* dst, size_t cap, void* stream) {

@@ -218,12 +218,9 @@ void free_all(dlq_resnet18* m) {
 
 float inv_scale(float s) { return 1.0f / s; }
 
-// DLQ_HEAD_SPLIT=1 (read at every call): GAP and FC as two launches
-// (gap16_kernel + linear_kernel) instead of the fused gap_fc_kernel.
-bool head_split() {
-  const char* e = std::getenv("DLQ_HEAD_SPLIT");
-  return e && e[0] == '1';
-}
+// Knob "head_split" (DLQ_HEAD_SPLIT=1, dlq_set_knob): GAP and FC as two
+// launches (gap16_kernel + linear_kernel) instead of the fused gap_fc_kernel.
+bool head_split() { return g_knob_head_split.load(std::memory_order_relaxed) == 1; }
 
 // conv2d_nchw_im2col_gemm + bn_launch (+ add_inplace + relu_forward) of the
 // reference, as one implicit-GEMM launch with the epilogue fused.
@@ -969,14 +966,13 @@ bool use_split(const dlq_resnet18* m, int B) {
   return on && m->prec == DLQ_PREC_INT8 && !m->timing && !m->keep && B >= 64;
 }
 
-// Replay the forward as a hipGraph?  Only with DLQ_GRAPH=1 (read at every
-// call): measured at B=256 the replay is ~1 % SLOWER than the 16 direct
-// launches (409k vs 414k images/s, same box), so direct launches are the
-// default.  Never while timing launches (events between launches) or
+// Replay the forward as a hipGraph?  Only with knob "graph" = 1 (DLQ_GRAPH=1
+// or dlq_set_knob): measured at B=256 the replay is ~1 % SLOWER than the 16
+// direct launches (409k vs 414k images/s, same box), so direct launches are
+// the default.  Never while timing launches (events between launches) or
 // keeping stage dumps (host-side copies).
 bool use_graph(const dlq_resnet18* m) {
-  const char* e = std::getenv("DLQ_GRAPH");
-  return e && e[0] == '1' && !m->timing && !m->keep;
+  return g_knob_graph.load(std::memory_order_relaxed) == 1 && !m->timing && !m->keep;
 }
 
 int forward_graph(dlq_resnet18* m, const float* x, int B, float* logits, hipStream_t s) {

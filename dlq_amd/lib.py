@@ -41,6 +41,8 @@ _SIGS = {
     "dlq_version": ([], C.c_char_p),
     "dlq_last_error": ([], C.c_char_p),
     "dlq_device_arch": ([_i, C.c_char_p, _i], _i),
+    "dlq_set_knob": ([C.c_char_p, _i], _i),
+    "dlq_get_knob": ([C.c_char_p, C.POINTER(_i)], _i),
     "dlq_quantize_weights_s8": ([_vp, _i, _i, _vp, _vp], _i),
     "dlq_fold_bn": ([_f, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp], _i),
     "dlq_res_scale": ([_f, _f], _f),
@@ -142,6 +144,19 @@ def last_error() -> str:
 def check(rc: int, what: str = "dlq") -> None:
     if rc != DLQ_OK:
         raise DLQError(f"{what} failed (code {rc}): {last_error()}")
+
+
+def get_knob(name: str) -> int:
+    v = C.c_int(0)
+    check(lib.dlq_get_knob(name.encode(), C.byref(v)), f"get_knob({name})")
+    return v.value
+
+
+def set_knob(name: str, value: int) -> int:
+    """Set a process-wide knob (include/dlq.h dlq_set_knob); returns the old value."""
+    old = get_knob(name)
+    check(lib.dlq_set_knob(name.encode(), int(value)), f"set_knob({name})")
+    return old
 
 
 def ptr(t) -> int | None:

@@ -107,6 +107,18 @@ int dlq_pack_conv_weights_s8(const dlq_conv_desc* d, const int8_t* q_oihw, int I
 /* status.  The NHWC operators further below are the fast path.              */
 /* ------------------------------------------------------------------------ */
 
+/* Process-wide test / A-B knobs, read on the host at each forward without
+ * touching the environment (each starts from its environment variable,
+ * read ONCE when the library loads; no reference counterpart):
+ *   "l1_grid"    (DLQ_L1_GRID)    cap on the layer1 block's grid, 0 = one
+ *                                 workgroup per CU (>0 puts several images in
+ *                                 one workgroup);
+ *   "head_split" (DLQ_HEAD_SPLIT) 1 = GAP and FC as two launches;
+ *   "graph"      (DLQ_GRAPH)      1 = replay the forward as a hipGraph.
+ * Returns DLQ_ERR_ARG for an unknown name. */
+int dlq_set_knob(const char* name, int value);
+int dlq_get_knob(const char* name, int* value);
+
 /* Select the device and check it is gfx950 (the kernels' only target).    */
 int dlq_init(int device);
 /* Synchronise the device; pairs with dlq_init.                            */

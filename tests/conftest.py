@@ -20,3 +20,18 @@ def gpu():
         pytest.skip("no GPU visible")
     from dlq_amd import lib  # raises loudly if libdlq.so is missing
     return lib
+
+
+@pytest.fixture
+def knobs():
+    """Set libdlq knobs (dlq_set_knob) for one test; restored afterwards."""
+    from dlq_amd import lib as L
+    saved = {}
+
+    def set_(name, value):
+        old = L.set_knob(name, value)
+        saved.setdefault(name, old)
+
+    yield set_
+    for name, old in saved.items():
+        L.set_knob(name, old)

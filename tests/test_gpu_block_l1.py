@@ -21,7 +21,7 @@ def _layer(rng, s_x, s_y):
     return wq, alpha, beta, packed
 
 
-def _run(N, seed, lo, grid=None, monkeypatch=None):
+def _run(N, seed, lo, grid=None, knobs=None):
     from dlq_amd import ops
     rng = np.random.default_rng(seed)
     s_x, s_h, s_y = np.float32(0.03), np.float32(0.05), np.float32(0.06)
@@ -32,7 +32,7 @@ def _run(N, seed, lo, grid=None, monkeypatch=None):
     h = O.epilogue_s8(O.conv_s8_acc(x, wq1, 1, 1), a1, b1, relu=True)
     ref = O.epilogue_s8(O.conv_s8_acc(h, wq2, 1, 1), a2, b2, res=x, r_s=r_s, relu=True)
     if grid is not None:
-        monkeypatch.setenv("DLQ_L1_GRID", str(grid))
+        knobs("l1_grid", grid)
     cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
     y = ops.block_l1_s8(cu(nchw_to_nhwc(x)), cu(p1), cu(a1), cu(b1), cu(p2), cu(a2), cu(b2), float(r_s))
     torch.cuda.synchronize()
@@ -45,10 +45,10 @@ def test_block_l1_bitexact(gpu, N, lo):
     assert np.array_equal(got, ref)
 
 
-def test_block_l1_several_images_per_workgroup(gpu, monkeypatch):
+def test_block_l1_several_images_per_workgroup(gpu, knobs):
     """Grid capped at 2 workgroups: images 0,2,4 and 1,3 each run as one
     stream of rows through the LDS rings (image boundaries inside a phase)."""
-    got, ref = _run(5, 7, 0, grid=2, monkeypatch=monkeypatch)
+    got, ref = _run(5, 7, 0, grid=2, knobs=knobs)
     assert np.array_equal(got, ref)
 
 

@@ -193,14 +193,14 @@ def test_stem_fused_f8_within_bound(gpu, N):
 
 
 @pytest.mark.parametrize("N,grid", [(3, None), (5, "2")])
-def test_block_l1_f8_equals_two_convs(gpu, N, grid, monkeypatch):
+def test_block_l1_f8_equals_two_convs(gpu, N, grid, knobs):
     """The fused layer1 block groups each tap's 64 channels into one MFMA in
     the same lane order and tap order as the generic conv kernel, so it is
     bit-identical to two dlq_conv2d_nhwc_f8 calls (which the oracle checks);
-    grid "2" puts several images in one workgroup (the DLQ_L1_GRID knob)."""
+    grid "2" puts several images in one workgroup (the "l1_grid" knob)."""
     from dlq_amd import ops
     if grid:
-        monkeypatch.setenv("DLQ_L1_GRID", grid)
+        knobs("l1_grid", int(grid))
     rng = np.random.default_rng(53 + N)
     x = O.quantize_f32_f8(np.abs(rng.standard_normal((N, 56, 56, 64))).astype(np.float32) * 30, 1.0)
     ws, al, be = [], [], []

@@ -256,14 +256,14 @@ def test_gap_fc_rejects_unsupported_shapes(gpu):
         ops.gap_fc_s8(torch.zeros((2, 7, 7, 256), dtype=torch.int8, device="cuda"), 0.1, w, 1000, v, v)
 
 
-def test_resnet18_fused_head_matches_split_head(gpu, monkeypatch):
-    """B=256 forward with the fused head (default) == DLQ_HEAD_SPLIT=1."""
+def test_resnet18_fused_head_matches_split_head(gpu, knobs):
+    """B=256 forward with the fused head (default) == knob head_split = 1."""
     from dlq_amd.models import ResNet18Int8, synthetic_images
     sd, scales = model_and_scales()
     x = synthetic_images(256, seed=21).cuda()
     model = ResNet18Int8(sd, scales, max_batch=256)
     fused = model(x).cpu().numpy()
-    monkeypatch.setenv("DLQ_HEAD_SPLIT", "1")
+    knobs("head_split", 1)
     split = model(x).cpu().numpy()
     assert np.array_equal(fused.view(np.int32), split.view(np.int32))
 
@@ -322,13 +322,13 @@ def test_resnet18_batch_invariance_full_batch(gpu):
     assert np.array_equal(ref.view(np.int32), big[[0, 255]].view(np.int32))
 
 
-def test_resnet18_graph_replay_matches_launches(gpu, monkeypatch):
+def test_resnet18_graph_replay_matches_launches(gpu, knobs):
     """The forward is captured once per (x, B, logits) into a hipGraph and
-    replayed (DLQ_GRAPH=1): a replay over NEW contents of the same input
+    replayed (knob graph = 1, DLQ_GRAPH=1): a replay over NEW contents of the same input
     buffer, and a re-capture for another batch size, equal the kernel-by-
     kernel forward (the default) bit for bit."""
     from dlq_amd.models import ResNet18Int8, synthetic_images
-    monkeypatch.setenv("DLQ_GRAPH", "1")
+    knobs("graph", 1)
     sd, scales = model_and_scales()
     model = ResNet18Int8(sd, scales, max_batch=64)
     x = synthetic_images(64, seed=3).cuda()
@@ -338,7 +338,7 @@ def test_resnet18_graph_replay_matches_launches(gpu, monkeypatch):
         x.copy_(synthetic_images(64, seed=seed).cuda())
         got.append(model(x, out=out).cpu().numpy())
     small = model(x[:5], out=out[:5]).cpu().numpy()  # another (x, B, logits): re-capture
-    monkeypatch.setenv("DLQ_GRAPH", "0")
+    knobs("graph", 0)
     ref = model(x).cpu().numpy()
     x.copy_(synthetic_images(64, seed=3).cuda())
     ref0 = model(x).cpu().numpy()
@@ -415,12 +415,16 @@ def test_mnist_mlp_bitexact(gpu, hidden):
 
 
 @pytest.mark.parametrize("inp,hidden,out,B", [(100, 64, 10, 50), (784, 192, 10, 1000), (257, 512, 37, 33),
-                                              (784, 1024, 10, 64), (130, 128, 3, 17)])
+                                              (784, 1024, 10, 64), (130, 128, 3, 17),
+                                              (784, 8192, 10, 40), (16384, 256, 10, 9)])
 def test_mlp_fused_shapes_bitexact(gpu, inp, hidden, out, B):
     """The one-launch MLP (head.hip mlp_fused_kernel) off the MNIST shape: `in`
     not a multiple of 4 or 64 (scalar loads, zero K tail), K split over waves
     (hidden < 256) or several tiles per wave (hidden > 256), more than one fc2
-    tile, ragged row blocks -- int32 sums and epilogues bit-exact vs the oracle."""
+    tile, ragged row blocks -- int32 sums and epilogues bit-exact vs the oracle.
+    The last two shapes need more than the fused kernel's 64 KiB of LDS
+    (hidden 8192; in 16384): dlq_mlp_forward runs them as quantize_rows + two
+    linear launches, with the same bits."""
     from dlq_amd.models import MLPInt8, mlp_weights
     from dlq_amd.quant import calibrate_mlp
     W1, b1, W2, b2 = mlp_weights(inp, hidden, out, seed=inp + hidden)
