@@ -156,8 +156,8 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: roles branch on SGPRs
   const int lr = lane & 31, lh = lane >> 5;
   const bool second = wave >= 4;  // conv2 wave
-  const int NG = gridDim.x, b = blockIdx.x;
-  const int J = (a.N - b + NG - 1) / NG;  // images b, b+NG, ... of this workgroup
+  int i0, J;
+  xcd_chunk(a.N, i0, J);  // this workgroup's images: xcd_item(i0, 0 .. J-1)
   const int rows = J * LW;
   const int nphase = rows / RPH + 2;  // conv2 trails conv1 by 9 rows
   const unsigned lds32 = lds_addr32(lds);
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
   auto row_src = [&](int R) -> const int8_t* {
     if (R < 0 || R >= rows) return nullptr;
     const int j = R / LW, r = R - j * LW;
-    return a.x + ((size_t)(b + j * NG) * LW + r) * (LW * LC);
+    return a.x + ((size_t)xcd_item(i0, j) * LW + r) * (LW * LC);
   };
   const bool pix_lane = lane >= 1 && lane <= LW;
   auto dma_piece = [&](int R, int p) {
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
           int s0 = S_mid + ro;
           if (s0 >= NR) s0 -= NR;
           row_addrs(OFF_MID, s0, r, col, valid, ra[t]);
-          const size_t pix = valid ? ((size_t)(b + jm * NG) * LW + r) * LW + col : 0;
+          const size_t pix = valid ? ((size_t)xcd_item(i0, jm) * LW + r) * LW + col : 0;
           if constexpr (BL1_TEST == 7)
             rq[t] = v4i{0, 0, 0, 0};
           else
@@ -481,7 +481,8 @@ template <bool SECOND>
 __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds, unsigned lds32, int wave, int rows,
                                                  int nphase) {
   const int lane = threadIdx.x & 63, lr = lane & 31, lh = lane >> 5;
-  const int NG = gridDim.x, b = blockIdx.x;
+  int i0, nimg;
+  xcd_chunk(a.N, i0, nimg);  // this workgroup's images: xcd_item(i0, 0 .. nimg-1)
   const int h = wave & 1, par = (wave >> 1) & 1;  // output-channel half, tile parity
   v4i wr[KS];
   const int8_t* ws = SECOND ? a.w2 : a.w1;
@@ -506,7 +507,7 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
   auto row_src = [&](int R) -> const int8_t* {
     if (R < 0 || R >= rows) return nullptr;
     const int j = R / LW, r = R - j * LW;
-    return a.x + ((size_t)(b + j * NG) * LW + r) * (LW * LC);
+    return a.x + ((size_t)xcd_item(i0, j) * LW + r) * (LW * LC);
   };
   const bool pix_lane = lane >= 1 && lane <= LW;
   auto dma_piece = [&](int R, int p) {
@@ -621,7 +622,7 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
         int s0 = S_mid2 + ro;
         if (s0 >= NR) s0 -= NR;
         row_addrs(OFF_MID, s0, r, col, valid, jb.ra);
-        const size_t pix = valid ? ((size_t)(b + jm * NG) * LW + r) * LW + col : 0;
+        const size_t pix = valid ? ((size_t)xcd_item(i0, jm) * LW + r) * LW + col : 0;
         jb.rq = *(const v4i*)(a.x + pix * LC + h * 32 + lh * 16);
         jb.dst = valid ? a.y + pix * LC + h * 32 + lh * 16 : g_trash_b + lane * 16;
       }
@@ -725,8 +726,8 @@ __global__ __launch_bounds__(512, 1) void block_l1_sp_kernel(BlockArgs a) {
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int NG = gridDim.x, b = blockIdx.x;
-  const int J = (a.N - b + NG - 1) / NG;  // images b, b+NG, ... of this workgroup
+  int i0, J;
+  xcd_chunk(a.N, i0, J);  // this workgroup's images (device_common.h xcd_chunk)
   const int rows = J * LW;
   const int nphase = rows / RPH + 1;  // conv2 trails conv1 by 9 rows; its last phase takes 9
   for (int i = tid; i < RING / 16; i += 512) *(v4i*)(lds + OFF_MID + 16 * i) = v4i{0, 0, 0, 0};

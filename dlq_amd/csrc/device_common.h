@@ -1,5 +1,7 @@
 // device_common.h -- device-side types and helpers shared by the gfx950 kernels.
 #pragma once
+#include <type_traits>
+
 #include "dlq_internal.h"
 
 namespace dlq {
@@ -156,12 +158,47 @@ __device__ __forceinline__ unsigned epi4_res_f8(const float* acc, const float* a
   return enc4_f8(y01[0], y01[1], y23[0], y23[1], lo);
 }
 
+// Compile-time unrolled loop: f(std::integral_constant<int, I>) for I in [B, E).
+template <int B, int E, typename F>
+__device__ __forceinline__ void for_c(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    for_c<B + 1, E>(f);
+  }
+}
+
 // Bijective XCD-aware remap: consecutive logical tiles land on one XCD
 // (cdna_hip_programming.md §5 "XCD swizzle must be bijective").
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
   const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   return base + (bid >> 3);
+}
+
+// Work split of a launch's n_items over its blocks: logical block b =
+// xcd_remap(blockIdx.x) takes items b, b + gridDim, ... (count of them).
+// -DDLQ_X_XCDIMG instead gives b the contiguous range [first, first + count)
+// of a balanced partition, so that XCD x works on the same eighth of the
+// batch in every layer (an attempt to serve each layer's input from the L2
+// that wrote it: no gain on the wide convs, the stride-2 convs 1.5-2 us
+// slower per launch, tools/ab.py on one box).
+__device__ __forceinline__ void xcd_chunk(int n_items, int& first, int& count) {
+  const int Gd = gridDim.x, b = xcd_remap(blockIdx.x, Gd);
+#ifdef DLQ_X_XCDIMG
+  first = (int)((long long)b * n_items / Gd);
+  count = (int)((long long)(b + 1) * n_items / Gd) - first;
+#else
+  first = b;
+  count = n_items > b ? (n_items - b + Gd - 1) / Gd : 0;
+#endif
+}
+// item index of the block's li-th item under xcd_chunk
+__device__ __forceinline__ int xcd_item(int first, int li) {
+#ifdef DLQ_X_XCDIMG
+  return first + li;
+#else
+  return first + li * (int)gridDim.x;
+#endif
 }
 
 // One 16-byte LDS-DMA per lane: global (per-lane address) -> LDS at the
@@ -210,6 +247,14 @@ __device__ __forceinline__ v4i gload16_untracked(const void* p) {
   v4i r;
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
   return r;
+}
+
+typedef int v2i __attribute__((ext_vector_type(2)));
+
+// ds_read_b64_tr_b8: per 16-lane group, lane 2q + p addresses row q (of 8),
+// bytes 8p .. 8p+7; lane i receives column i's 8 row bytes, byte q = row q.
+__device__ __forceinline__ v2i ds_tr8(const int8_t* p) {
+  return __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)p);
 }
 
 // MFMA-layout <-> store-layout exchange for a 32x32 int8 output tile (see

@@ -181,11 +181,6 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_generic_kernel(const int8
 
 __device__ __attribute__((aligned(64))) int8_t g_zero_gemm[64];
 
-typedef int v2i __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ v2i ds_tr8(const int8_t* p) {
-  return __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)p);
-}
 
 constexpr int GK2 = 128;
 constexpr int GSLOT2_A = GT * GK2;  // 32 KiB

@@ -155,7 +155,10 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
   const int cv_r = (tid >> 4) & 3, cv_u = (tid & 15) + 16 * (tid >> 6);
 
   ST_DECL;
-  for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+  int item0, n_my;
+  xcd_chunk(nitems, item0, n_my);
+  for (int li = 0; li < n_my; ++li) {
+    const int item = xcd_item(item0, li);
     const int n = item / a.nb, band = item - n * a.nb;
     const int py0 = band * a.R, py1 = min(56, py0 + a.R);
     if (py0 >= py1) continue;
@@ -552,7 +555,10 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
   const int8_t* tr1 = stg + R1 * 16 + 8 * ((ti & 1) ^ ((R1 >> 3) & 1));
   const int8_t* tr2 = stg + R2 * 16 + 8 * ((ti & 1) ^ ((R2 >> 3) & 1));
 
-  for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+  int item0, n_my;
+  xcd_chunk(nitems, item0, n_my);
+  for (int li = 0; li < n_my; ++li) {
+    const int item = xcd_item(item0, li);
     const int n = item / a.nb, band = item - n * a.nb;
     const int py0 = band * a.R, py1 = min(56, py0 + a.R);
     if (py0 >= py1) continue;

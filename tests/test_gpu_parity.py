@@ -146,6 +146,31 @@ def test_s2_conv_with_fused_downsample_bitexact(gpu, C, H, N):
     assert np.array_equal(got_d, ref_d), f"downsample: {np.count_nonzero(got_d != ref_d)} mismatches"
 
 
+@pytest.mark.parametrize("C,H", [(128, 28), (256, 14), (512, 7)])
+@pytest.mark.parametrize("residual", [False, True])
+def test_wide_conv_no_relu_bitexact(gpu, C, H, residual):
+    """The wide stride-1 kernel's signed requantisation (relu = 0: clamp
+    [-127, 127]) with and without a residual, ragged batch -- the forward only
+    runs the ReLU forms, the C-ABI takes either."""
+    from dlq_amd import ops
+    rng = np.random.default_rng(C + 3 * residual)
+    N = 3
+    x = rand_s8(rng, (N, C, H, H))
+    w, bn = rand_conv(rng, C, C, 3)
+    wq, sw = O.quantize_weights_s8(w)
+    s_x, s_y, s_r = 0.023, 0.06, 0.031  # ~1-3 % of the outputs at a clamp
+    alpha, beta = O.fold_bn(s_x, sw, bn, s_y)
+    r_s = O.res_scale(s_r, s_y)
+    res = rand_s8(rng, (N, C, H, H)) if residual else None
+    ref = O.epilogue_s8(O.conv_s8_acc(x, wq, 1, 1), alpha, beta, res, r_s, False)
+    assert ref.min() == -127 and ref.max() == 127  # both clamps exercised
+    xd, wd = _gpu_conv_inputs(x, wq, 1, 1)
+    y = ops.conv2d_nhwc_s8(xd, wd, C, 3, 1, 1, _cuda(alpha), _cuda(beta),
+                           residual=_cuda(nchw_to_nhwc(res)) if residual else None, res_scale=r_s, relu=False)
+    got = nhwc_to_nchw(y.cpu().numpy())
+    assert np.array_equal(got, ref), f"{np.count_nonzero(got != ref)} int8 mismatches"
+
+
 @pytest.mark.parametrize("C,H,N", [(128, 28, 90), (256, 14, 180), (512, 7, 360)])
 def test_wide_conv_many_items_per_workgroup(gpu, C, H, N):
     """Batches large enough that every workgroup of the wide stride-1 kernel
