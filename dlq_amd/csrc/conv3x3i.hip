@@ -196,8 +196,6 @@ struct WideStream {
     ot = it % n_ot;
     p0 = (it / n_ot) * IL;
   }
-  // does this loader wave issue DPW pieces per stage (else DPW - 1)?
-  __device__ __forceinline__ bool full() const { return wv + (DPW - 1) * NLD < G::NPIECE; }
   __device__ __forceinline__ void prep_issue(int li) {
     int ot, p0;
     item_of(li, ot, p0);
@@ -248,13 +246,11 @@ struct WideStream {
 
 // RELU (int8, OUT == 0): the output clamp is [0, 127] and the requantisation
 // takes the v_cvt_pk_u8_f32 form (device_common.h quant4_relu).
-// DSH: this wave's DMA schedule is rotated by DSH k-steps, so that the eight
-// waves do not all issue their LDS-DMA pieces at the same k-step.
-template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false, bool RELU = false, int DSH = 0>
+template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false, bool RELU = false>
 __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int mt, int f0, int lrank) {
   constexpr int SPS = sps_of<W, F8>();
   using G = IGeo<W, SPS>;
-  constexpr int H = W, NSL = C / ISC, NS = NSL / SPS;  // 32-channel slices, stages
+  constexpr int NS = C / ISC / SPS;  // stages (SPS 32-channel slices each)
   constexpr int KSN = 9 * SPS;                            // k-steps (tap, slice) per stage
   constexpr int OFF_AB = G::OFF_AB;
   constexpr int DPW = (G::NPIECE + NLD - 1) / NLD;  // pieces per loader wave per stage
@@ -445,8 +441,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #pragma unroll
     for (int ks = 0; ks < KSN; ++ks) {
       const int bu = ks & 1;
-      const int kr = (ks + KSN - DSH % KSN) % KSN;  // rotated DMA schedule
-      const int k0 = kr * DPW / KSN, k1 = (kr + 1) * DPW / KSN;
+      const int k0 = ks * DPW / KSN, k1 = (ks + 1) * DPW / KSN;
       if (dma) {
 #pragma unroll
         for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
@@ -492,8 +487,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     for (int ks = 0; ks < KSN; ++ks) {
       const int bu = ks & 1;
       if (ks + 1 < KSN) fa[bu ^ 1] = a_at(ks + 1);
-      const int kr = (ks + KSN - DSH % KSN) % KSN;  // rotated DMA schedule
-      const int k0 = kr * DPW / KSN, k1 = (kr + 1) * DPW / KSN;
+      const int k0 = ks * DPW / KSN, k1 = (ks + 1) * DPW / KSN;
       if (dma) {
 #pragma unroll
         for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
@@ -623,28 +617,6 @@ __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   int mt, f0, nf;
   const int wave = tid >> 6;
   wave_tiles<G::MT>(wave, mt, f0, nf);
-#ifdef DLQ_X_DSH
-  // wave w's DMA schedule rotated by dsh(w) k-steps (SIMD partners w, w + 4 apart)
-  constexpr int K = sps_of<W, F8>() * 9;
-  auto go = [&](auto wc) {
-    constexpr int w = decltype(wc)::value, DSH = ((w & 3) * 2 + (w >> 2)) * K / 8;
-    if constexpr (G::MT == 4)
-      conv3x3i_body<W, C, OUT, RES, w < 4 ? 7 : 6, 8, F8, RELU, DSH>(a, lds, mt, f0, wave);
-    else
-      conv3x3i_body<W, C, OUT, RES, (w >> 1) == 0 ? 4 : 3, 8, F8, RELU, DSH>(a, lds, mt, f0, wave);
-  };
-  switch (wave) {
-    case 0: go(std::integral_constant<int, 0>{}); break;
-    case 1: go(std::integral_constant<int, 1>{}); break;
-    case 2: go(std::integral_constant<int, 2>{}); break;
-    case 3: go(std::integral_constant<int, 3>{}); break;
-    case 4: go(std::integral_constant<int, 4>{}); break;
-    case 5: go(std::integral_constant<int, 5>{}); break;
-    case 6: go(std::integral_constant<int, 6>{}); break;
-    default: go(std::integral_constant<int, 7>{}); break;
-  }
-  (void)nf;
-#else
   if constexpr (G::MT == 4) {
     if (nf == 7)
       conv3x3i_body<W, C, OUT, RES, 7, 8, F8, RELU>(a, lds, mt, f0, wave);
@@ -655,271 +627,6 @@ __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
       conv3x3i_body<W, C, OUT, RES, 4, 8, F8, RELU>(a, lds, mt, f0, wave);
     else
       conv3x3i_body<W, C, OUT, RES, 3, 8, F8, RELU>(a, lds, mt, f0, wave);
-  }
-#endif
-}
-
-// ---- The tile-major int8 body (OUT == 0, every int8 forward launch) ------
-// Same items, stages, ring and DMA plan as conv3x3i_body; what changes is the
-// order of the MFMAs and where the epilogue runs.  All that wave's weight
-// fragments of a stage (9 taps x SPS slices) are read into registers at the
-// stage's start, and the MFMAs run tile by tile (the 9 * SPS k-steps of tile
-// f, then of tile f + 1), so in the item's last stage tile f's accumulators
-// are final after its chain and tile f's requantisation runs inside tile
-// f + 1's chain -- beside MFMAs instead of after the last one (only the last
-// tile's epilogue is left after the chains).
-// The accumulators are transposed, D[px][oc] (the pixel fragment is the MFMA's
-// A operand): a lane holds 16 pixels of ONE output channel, so its alpha/beta
-// are two registers instead of 32.  Store and residual go through a 1 KiB
-// per-wave LDS staging tile and ds_read_b64_tr_b8 (both transposes
-// conflict-free), so every global access is still one 16-byte NHWC chunk.
-constexpr int TSTG = 1024;  // per-wave epilogue staging bytes
-
-// residual staging row of pixel px: rows of even and odd 8-pixel groups are
-// interleaved (bit 2 flipped for odd groups) so that a transposed read's 8 rows
-// fall on 8 distinct bank octets
-__device__ __forceinline__ int res_row(int px) { return px ^ (((px >> 3) & 1) << 2); }
-
-template <int W, int C, bool RES, int NF, bool RELU>
-__device__ __forceinline__ void conv3x3t_body(const ConvArgs& a, int8_t* lds, int mt, int f0, int wave) {
-  constexpr int SPS = sps_of<W, false>();
-  using G = IGeo<W, SPS>;
-  using S = WideStream<W, C, SPS, INW>;
-  constexpr int NS = S::NS, KSN = 9 * SPS, NM = NF * KSN, DPW = S::DPW;
-  constexpr int NMD = (NF - 1) * KSN;  // the last stage issues its DMA during chains 0 .. NF-2
-  static_assert(NS >= 2, "an item = one or more accumulate-only stages + the last stage");
-  static_assert(DPW <= NMD, "at most one DMA piece per MFMA");
-  // stores after the last DMA piece of an item's last stage (epilogues of
-  // tiles NF-3 .. NF-1): all older VM ops are done at the next barrier
-  constexpr int STORES = NF < 3 ? NF : 3;
-  constexpr int EPI_VALU = RES ? 80 : 56;  // VALU per tile epilogue (16 values), spread over the next chain
-  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 31, lh = lane >> 5;
-  S st(a, lds, wave);
-  const int nst = st.nst;
-
-  // per px tile the slot-0 offsets of its kw = 0 / 1 / 2 taps (as conv3x3i_body)
-  const int a_row = (mt * 32 + lr) * IPITCH + lh * 16;
-  int col_off[3][NF];
-#pragma unroll
-  for (int f = 0; f < NF; ++f) {
-    int lp = (f0 + f) * 32 + lr;
-    lp = lp < IL ? lp : IL - 1;
-    const int c = lp / (G::RPI * W), rem = lp - c * (G::RPI * W);
-    const int r = rem / W, ow = rem - r * W;
-    const int bu = c * G::CS + r * G::RW + ow;
-    const int mid = G::OFF_P + lh * G::UP * 16 + bu * 16;
-    col_off[1][f] = mid;
-    col_off[0][f] = ow == 0 ? G::OFF_Z + ((bu - 1) & 15) * 16 : mid - 16;
-    col_off[2][f] = ow == W - 1 ? G::OFF_Z + ((bu + 1) & 15) * 16 : mid + 16;
-  }
-
-  // epilogue staging (see the file's transposes) and its fixed lane addresses
-  int8_t* stg = lds + 2 * G::SLOT + wave * TSTG;
-  const float* lds_ab = (const float*)(lds + 2 * G::SLOT + INW * TSTG);  // alpha[C], beta[C]
-  const int tg = lane >> 4, tj = lane & 15, tq = tj >> 1, tp = tj & 1;
-  // output: lane writes q[g] (pixels 8g + 4lh .. +3 of oc lr) at row lr, dword (2g + lh) ^ 2((lr >> 2) & 3)
-  const int o_swz = 2 * ((lr >> 2) & 3);
-  // transposed reads of the output: oc rows 16 (tg >> 1) + 8r + tq, pixel columns 16 (tg & 1) + 8 tp
-  const int8_t* o_rd[2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int oc = 16 * (tg >> 1) + 8 * r + tq;
-    o_rd[r] = stg + oc * 32 + 4 * ((4 * (tg & 1) + 2 * tp) ^ (2 * ((oc >> 2) & 3)));
-  }
-  // residual: lane (px lr, half lh) writes its 16 bytes at row res_row(lr);
-  // transposed reads: pixel rows 8 (2r + (tq >> 2)) + 4 (tg >> 1) + (tq & 3), oc columns 16 (tg & 1) + 8 tp
-  const int8_t* r_wr = stg + res_row(lr) * 32 + 16 * (lh ^ ((res_row(lr) >> 2) & 1));
-  const int8_t* r_rd[2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int px = 8 * (2 * r + (tq >> 2)) + 4 * (tg >> 1) + (tq & 3), row = res_row(px);
-    r_rd[r] = stg + row * 32 + 16 * ((tg & 1) ^ ((row >> 2) & 1)) + 8 * tp;
-  }
-
-  v16i acc[NF];
-  v4i rq[3];  // residual ring: tile t's in rq[t % 3], loaded two chains ahead of its epilogue
-  float al = 0.f, be = 0.f;  // this lane's output channel's, read from LDS in an item's last stage
-  int cur_ot = 0, cur_p0 = 0;
-
-  // residual of tile f in store layout.  Tracked loads: the compiler's vmcnt
-  // for rq counts only its own (younger rq loads, stores), so it also drains
-  // the DMA pieces issued in between -- conservative, never short, and
-  // those pieces were issued a chain or more earlier.
-  auto res_ld = [&](int f) {
-    const int p = cur_p0 + (f0 + f) * 32 + lr;
-    const bool keep = (f0 + f) * 32 + lr < IL && p < a.P;
-    rq[f % 3] = *(const v4i*)(a.res + (keep ? (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16 : 0));
-  };
-  // the epilogue of tile f (its accumulators final), NHWC int8 out
-  auto epi = [&](int f) {
-    const float r_s = a.s_res;
-    unsigned rr[4] = {0, 0, 0, 0};
-    if constexpr (RES) {
-      *(v4i*)r_wr = rq[f % 3];
-      const v2i r0 = ds_tr8(r_rd[0]), r1 = ds_tr8(r_rd[1]);
-      rr[0] = (unsigned)r0[0];
-      rr[1] = (unsigned)r0[1];
-      rr[2] = (unsigned)r1[0];
-      rr[3] = (unsigned)r1[1];
-    }
-    unsigned q[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int ac[4] = {acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
-      const float a4[4] = {al, al, al, al}, b4[4] = {be, be, be, be};
-      if constexpr (RELU && RES)
-        q[g] = epi4_res_relu(ac, a4, b4, rr[g], r_s);
-      else if constexpr (RELU)
-        q[g] = epi4_relu(ac, a4, b4);
-      else if constexpr (RES)
-        q[g] = epi4_res(ac, a4, b4, rr[g], r_s, a.relu ? 0.f : -127.f);
-      else
-        q[g] = epi4(ac, a4, b4, a.relu ? 0.f : -127.f);
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) *(unsigned*)(stg + lr * 32 + 4 * ((2 * g + lh) ^ o_swz)) = q[g];
-    const v2i o0 = ds_tr8(o_rd[0]), o1 = ds_tr8(o_rd[1]);
-    const int lp = (f0 + f) * 32 + lr, p = cur_p0 + lp;
-    const bool keep = lp < IL && p < a.P;
-    v4i* dst = keep ? (v4i*)((int8_t*)a.y + (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16)
-                    : (v4i*)(g_trash_i + lane * 16);
-    *dst = v4i{o0[0], o0[1], o1[0], o1[1]};
-  };
-
-  // one stage: weight fragments to registers, tile-major MFMA chains, the
-  // next stage's DMA spread over them; LAST: the epilogues inside the chains
-  auto stage = [&](int s, auto last_c, bool dma) {
-    constexpr bool LAST = decltype(last_c)::value;
-    constexpr int NMI = LAST ? NMD : NM;  // MFMAs the DMA pieces are spread over
-    const int sb = (s & 1) * G::SLOT;
-    const int8_t* abase = lds + sb + a_row;
-    v4i fa[KSN];
-#pragma unroll
-    for (int ks = 0; ks < KSN; ++ks) fa[ks] = *(const v4i*)(abase + (ks / 9) * G::WB + (ks % 9) * 32);
-    if constexpr (LAST && RES) res_ld(0);
-    if constexpr (LAST) {
-      const int oc = cur_ot * G::OT + mt * 32 + lr;
-      al = lds_ab[oc];
-      be = lds_ab[C + oc];
-    }
-    auto b_ld = [&](int i) -> v4i {
-      const int f = i / KSN, ks = i - f * KSN, tap = ks % 9;
-      return *(const v4i*)(lds + col_off[tap % 3][f] + (tap / 3) * G::RW * 16 + (ks / 9) * G::PB);
-    };
-    v4i fb[3];
-    fb[0] = b_ld(0);
-    fb[1] = b_ld(1);
-    __builtin_amdgcn_sched_barrier(0);  // the stage's fragment reads stay ahead of the chains
-    for_c<0, NF>([&](auto fc) {
-      constexpr int f = decltype(fc)::value;
-      if constexpr (LAST && RES && f + 1 < NF) res_ld(f + 1);
-#pragma unroll
-      for (int ks = 0; ks < KSN; ++ks) {
-        const int i = f * KSN + ks;
-        acc[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb[i % 3], fa[ks], acc[f], 0, 0, 0);
-        if (i + 2 < NM) fb[(i + 2) % 3] = b_ld(i + 2);
-        if (dma && i < NMI) {
-#pragma unroll
-          for (int k = i * DPW / NMI; k < (i + 1) * DPW / NMI; ++k) st.issue(s + 1, k);
-        }
-      }
-      if constexpr (LAST && f >= 1) epi(f - 1);
-      // per MFMA: the MFMA, the B fragment two ahead, (a DMA piece), and an
-      // equal share of the previous tile's epilogue VALU
-#pragma unroll
-      for (int ks = 0; ks < KSN; ++ks) {
-        const int i = f * KSN + ks;
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        if (i + 2 < NM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-        if (i < NMI && (i + 1) * DPW / NMI > i * DPW / NMI)
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (LDS-DMA)
-        if (LAST && f >= 1) __builtin_amdgcn_sched_group_barrier(0x002, EPI_VALU / KSN + 1, 0);  // VALU
-      }
-    });
-    if constexpr (LAST) epi(NF - 1);
-  };
-
-  ISTAMP(0);
-  st.prep_for(0);
-#pragma unroll
-  for (int k = 0; k < DPW; ++k) st.issue(0, k);
-  for (int i = tid; i < G::ZU * 4; i += INW * 64) {
-#pragma unroll
-    for (int sub = 0; sub < SPS; ++sub) {
-      ((int*)(lds + G::OFF_Z + sub * G::PB))[i] = 0;
-      ((int*)(lds + G::SLOT + G::OFF_Z + sub * G::PB))[i] = 0;
-    }
-  }
-  for (int i = tid; i < a.OCp; i += INW * 64) {  // published by stage 0's barrier
-    ((float*)lds_ab)[i] = a.alpha[i];
-    ((float*)lds_ab)[C + i] = a.beta[i];
-  }
-  // stage s's barrier (its DMA has landed; every wave is done with slot s - 1)
-  auto open_stage = [&](int s, int j) {
-    if (j == 0 && s > 0)
-      wait_vm_const<STORES>();
-    else
-      wait_vm_const<0>();
-    __builtin_amdgcn_s_barrier();
-    ISTAMP(1 + 2 * s);
-    if (s + 1 < nst) st.prep_for(s + 1);
-    if (s > 0) {
-      const int d = (s & 1) ? G::SLOT : -G::SLOT;
-#pragma unroll
-      for (int f = 0; f < NF; ++f) {
-        col_off[0][f] += d;
-        col_off[1][f] += d;
-        col_off[2][f] += d;
-      }
-    }
-  };
-  const std::integral_constant<bool, false> MID;
-  const std::integral_constant<bool, true> LASTC;
-  // items in sequence: NS - 1 stages that only accumulate, then the last one
-  // with the epilogues (one code path each, so acc[] is never merged over
-  // branches)
-  for (int li = 0, s = 0; li < st.nit; ++li) {
-    open_stage(s, 0);
-    st.item_of(li, cur_ot, cur_p0);
-#pragma unroll
-    for (int f = 0; f < NF; ++f) acc[f] = v16i{0};
-    stage(s, MID, true);
-    ISTAMP(2 + 2 * s);
-    ++s;
-    for (int j = 1; j < NS - 1; ++j, ++s) {
-      open_stage(s, j);
-      stage(s, MID, true);
-      ISTAMP(2 + 2 * s);
-    }
-    open_stage(s, NS - 1);
-    stage(s, LASTC, s + 1 < nst);
-    ISTAMP(2 + 2 * s);
-    ++s;
-  }
-  ISTAMP(62);
-  wait_vm0();
-  ISTAMP(63);
-}
-
-template <int W, int C, bool RES, bool RELU>
-__global__ __launch_bounds__(INW * 64, 1) void conv3x3t_kernel(ConvArgs a) {
-  using G = IGeo<W, sps_of<W, false>()>;
-  constexpr int LDS_TOTAL = 2 * G::SLOT + INW * TSTG + 2 * C * 4;
-  static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
-  __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
-  int mt, f0, nf;
-  const int wave = threadIdx.x >> 6;
-  wave_tiles<G::MT>(wave, mt, f0, nf);
-  if constexpr (G::MT == 4) {
-    if (nf == 7)
-      conv3x3t_body<W, C, RES, 7, RELU>(a, lds, mt, f0, wave);
-    else
-      conv3x3t_body<W, C, RES, 6, RELU>(a, lds, mt, f0, wave);
-  } else {
-    if (nf == 4)
-      conv3x3t_body<W, C, RES, 4, RELU>(a, lds, mt, f0, wave);
-    else
-      conv3x3t_body<W, C, RES, 3, RELU>(a, lds, mt, f0, wave);
   }
 }
 
@@ -941,16 +648,6 @@ hipError_t launch_ci(const ConvArgs& a, hipStream_t s) {
   const dim3 grid(NI < ncu ? NI : ncu), block(INW * 64);
   if (a.out_kind == 2)
     hipLaunchKernelGGL((conv3x3i_kernel<W, C, 2, false, F8>), grid, block, 0, s, a);
-#ifdef DLQ_X_TMWIDE
-  else if (!F8 && a.relu && a.res)
-    hipLaunchKernelGGL((conv3x3t_kernel<W, C, true, true>), grid, block, 0, s, a);
-  else if (!F8 && a.relu)
-    hipLaunchKernelGGL((conv3x3t_kernel<W, C, false, true>), grid, block, 0, s, a);
-  else if (!F8 && a.res)
-    hipLaunchKernelGGL((conv3x3t_kernel<W, C, true, false>), grid, block, 0, s, a);
-  else if (!F8)
-    hipLaunchKernelGGL((conv3x3t_kernel<W, C, false, false>), grid, block, 0, s, a);
-#endif
   else if (!F8 && a.relu && a.res)
     hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, true, F8, true>), grid, block, 0, s, a);
   else if (!F8 && a.relu)

@@ -151,7 +151,7 @@ __device__ __forceinline__ int perm_at(int slot) {
 // RELU (int8, OUT == 0): conv1's clamp is [0, 127], requantised in the
 // v_cvt_pk_u8_f32 form (device_common.h quant4_relu); the downsample keeps
 // the signed clamp.
-template <int OW, int C, int OUT, bool DS, int NF, bool F8, bool RW, bool RELU = false, int DSH = 0>
+template <int OW, int C, int OUT, bool DS, int NF, bool F8, bool RW, bool RELU = false>
 __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, const float* be_ds,
                                          int8_t* y_ds, int8_t* lds, int mt, int f0) {
   using G = JGeo<OW, DS, RW ? C / JSC : 0>;
@@ -414,8 +414,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
       if constexpr (DS) {
         if (tap == 3) fd = *(const v4i*)(lds + wb + d_row);  // the downsample's A fragment, used at tap 4
       }
-      const int kr = (tap + 9 - DSH % 9) % 9;  // this wave's rotated DMA schedule
-      const int k0 = kr * DPW / 9, k1 = (kr + 1) * DPW / 9;
+      const int k0 = tap * DPW / 9, k1 = (tap + 1) * DPW / 9;
       if (more && !DLQ_ABL(a, 2)) {  // probe builds: timing without the DMA
 #pragma unroll
         for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
@@ -534,27 +533,10 @@ __global__ __launch_bounds__(JNW * 64, 1) void conv3x3s2i_kernel(ConvArgs a, con
   static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
   const int wave = threadIdx.x >> 6;
-#ifdef DLQ_X_DSH
-  auto go = [&](auto wc) {  // wave w's DMA schedule rotated by dsh(w) taps
-    constexpr int w = decltype(wc)::value, DSH = ((w & 3) * 2 + (w >> 2)) * 9 / 8;
-    s2i_body<OW, C, OUT, DS, w < 4 ? 4 : 3, F8, RW, RELU, DSH>(a, w_ds, al_ds, be_ds, y_ds, lds, w & 3, w < 4 ? 0 : 4);
-  };
-  switch (wave) {
-    case 0: go(std::integral_constant<int, 0>{}); break;
-    case 1: go(std::integral_constant<int, 1>{}); break;
-    case 2: go(std::integral_constant<int, 2>{}); break;
-    case 3: go(std::integral_constant<int, 3>{}); break;
-    case 4: go(std::integral_constant<int, 4>{}); break;
-    case 5: go(std::integral_constant<int, 5>{}); break;
-    case 6: go(std::integral_constant<int, 6>{}); break;
-    default: go(std::integral_constant<int, 7>{}); break;
-  }
-#else
   if (wave < 4)
     s2i_body<OW, C, OUT, DS, 4, F8, RW, RELU>(a, w_ds, al_ds, be_ds, y_ds, lds, wave & 3, 0);
   else
     s2i_body<OW, C, OUT, DS, 3, F8, RW, RELU>(a, w_ds, al_ds, be_ds, y_ds, lds, wave & 3, 4);
-#endif
 }
 
 int num_cus_s2i() {

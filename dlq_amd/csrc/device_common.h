@@ -158,15 +158,6 @@ __device__ __forceinline__ unsigned epi4_res_f8(const float* acc, const float* a
   return enc4_f8(y01[0], y01[1], y23[0], y23[1], lo);
 }
 
-// Compile-time unrolled loop: f(std::integral_constant<int, I>) for I in [B, E).
-template <int B, int E, typename F>
-__device__ __forceinline__ void for_c(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    for_c<B + 1, E>(f);
-  }
-}
-
 // Bijective XCD-aware remap: consecutive logical tiles land on one XCD
 // (cdna_hip_programming.md §5 "XCD swizzle must be bijective").
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
