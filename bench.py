@@ -328,7 +328,7 @@ def extra_configs(dev):
     # the exported sgemm_tiled replacement (dlq_gemm_s8s8s32): int8 GEMM TOPS vs peak
     try:
         res = {}
-        for (M, N, K) in ((8192, 8192, 8192), (256, 50176, 2304)):
+        for (M, N, K) in ((8192, 8192, 8192), (256, 50176, 2304), (12544, 512, 4608)):
             A = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
             Bm = torch.randint(-127, 128, (K, N), dtype=torch.int8, device=dev)
             Cm = torch.empty((M, N), dtype=torch.int32, device=dev)
@@ -339,7 +339,10 @@ def extra_configs(dev):
             tops = 2.0 * M * N * K / (ms * 1e-3) / 1e12
             res[f"{M}x{N}x{K}"] = {"ms": round(ms, 4), "tops": round(tops, 1), "frac": round(tops / PEAK_I8_TOPS, 4)}
             del A, Bm, Cm
-        out["gemm_s8s8s32"] = {"kernel": "gemm_s8s8s32_k128_kernel (gemm.hip)", "peak_tops": round(PEAK_I8_TOPS, 1), **res}
+        out["gemm_s8s8s32"] = {"kernel": "gemm_s8s8s32_k128_kernel (gemm.hip), tile chosen by shape",
+                               "peak_tops": round(PEAK_I8_TOPS, 1),
+                               "shapes": "8192^3; the layer-conv shapes OC x pixels x K (256 x 50176 x 2304) and "
+                                         "pixels x OC x K (12544 x 512 x 4608)", **res}
     except Exception as e:
         out["gemm error"] = repr(e)
     # configs[4]: fp8 (e4m3) activations + per-channel e4m3 weights, B = 256

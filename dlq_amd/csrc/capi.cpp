@@ -123,6 +123,7 @@ int env_int(const char* name) {
 std::atomic<int> g_knob_l1_grid{env_int("DLQ_L1_GRID")};
 std::atomic<int> g_knob_head_split{env_int("DLQ_HEAD_SPLIT")};
 std::atomic<int> g_knob_graph{env_int("DLQ_GRAPH")};
+std::atomic<int> g_knob_gemm_tile{env_int("DLQ_GEMM_TILE")};
 
 namespace {
 std::atomic<int>* knob(const char* name) {
@@ -130,6 +131,7 @@ std::atomic<int>* knob(const char* name) {
   if (!std::strcmp(name, "l1_grid")) return &g_knob_l1_grid;
   if (!std::strcmp(name, "head_split")) return &g_knob_head_split;
   if (!std::strcmp(name, "graph")) return &g_knob_graph;
+  if (!std::strcmp(name, "gemm_tile")) return &g_knob_gemm_tile;
   return nullptr;
 }
 }  // namespace

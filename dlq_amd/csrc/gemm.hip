@@ -5,7 +5,10 @@
 // weights [OC][IC*kH*kW], B = im2col [IC*kH*kW][OH*OW]).  int32 sums are
 // exact, so any k order gives the reference's accumulators bit for bit.
 //
-// Tile 256 x 256 per 512-thread workgroup (8 waves = 2 (M) x 4 (N), each 128 x
+// Two kernels.  K % 16 == N % 16 == 0 (16-byte aligned bases): the LDS-DMA
+// kernel below (gemm_s8s8s32_k128_kernel, K = 128 per stage, tile 256 x 256,
+// 256 x 128 or 128 x 128 chosen by shape).  Otherwise the register-staged
+// kernel: tile 256 x 256 per 512-thread workgroup (8 waves = 2 (M) x 4 (N), each 128 x
 // 64 = 4 x 2 v_mfma_i32_32x32x32_i8 tiles), K = 64 per stage, double-buffered
 // LDS (2 x 40 KiB), one barrier per stage; global loads run two stages ahead
 // in two register sets, so each has two stages of MFMAs to land.
@@ -183,124 +186,172 @@ __device__ __attribute__((aligned(64))) int8_t g_zero_gemm[64];
 
 
 constexpr int GK2 = 128;
-constexpr int GSLOT2_A = GT * GK2;  // 32 KiB
-constexpr int GSLOT2 = GSLOT2_A + GK2 * GT;
 
-__global__ __launch_bounds__(512, 1) void gemm_s8s8s32_k128_kernel(const int8_t* __restrict__ A,
-                                                                  const int8_t* __restrict__ B,
-                                                                  int32_t* __restrict__ C, int M, int N, int K,
-                                                                  int nbn) {
-  __shared__ __attribute__((aligned(16))) int8_t lds[2 * GSLOT2];
+// Tile TM x TN per workgroup of WM x WN waves, each wave MI x NJ MFMA tiles
+// (32 x 32); TM = 32 WM MI, TN = 32 WN NJ.  Per stage K = 128: TM / 8 A
+// pieces (8 rows x 128 K bytes each) and TN / 8 B pieces (1024 / TN K rows x
+// TN bytes each), dealt to the waves round-robin.
+//  * A image: row m = 128 K bytes, chunk c at m*128 + 16*(c ^ ((m >> 1) & 7)).
+//  * B image: K rows of TN bytes as loaded: chunk b of row k at k*TN +
+//    16*(b ^ swz(k)), swz(k) = 2(k & 7) for TN = 256 and 2((k >> 1) & 3) for
+//    TN = 128 -- either way a ds_read_b64_tr_b8 half-wave's 8 rows x 32
+//    columns fall on 64 distinct banks, and swz(k + 8) = swz(k).
+template <int TN>
+__device__ __forceinline__ int bswz(int k) {
+  return TN == 256 ? 2 * (k & 7) : 2 * ((k >> 1) & 3);
+}
+
+template <int WM, int WN, int MI, int NJ, int WPS>
+__global__ __launch_bounds__(WM * WN * 64, WPS) void gemm_s8s8s32_k128_kernel(const int8_t* __restrict__ A,
+                                                                             const int8_t* __restrict__ B,
+                                                                             int32_t* __restrict__ C, int M, int N,
+                                                                             int K, int nbn) {
+  constexpr int NW = WM * WN, TM = 32 * WM * MI, TN = 32 * WN * NJ;
+  static_assert(TN == 256 || TN == 128, "B image swizzle");
+  constexpr int SA = TM * GK2, SLOT = SA + GK2 * TN;  // slot: A image, then B image
+  constexpr int PA = TM / 8, PB = TN / 8, NP = PA + PB, PPW = NP / NW;  // pieces: A, B, per wave
+  static_assert(NP % NW == 0 && PPW <= 4 * MI * NJ, "at most one piece per MFMA of a stage");
+  constexpr int CPR = TN / 16;  // B chunks per K row
+  __shared__ __attribute__((aligned(16))) int8_t lds[2 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 31, lh = lane >> 5;
   const int l = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (l / nbn) * GT, n0 = (l % nbn) * GT;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int m0 = (l / nbn) * TM, n0 = (l % nbn) * TN;
+  const int wm = wave / WN, wn = wave % WN;
   const unsigned lds32 = lds_addr32(lds);
   const int nst = (K + GK2 - 1) / GK2;
 
-  // 64 DMA pieces per stage: 32 for A (piece j = rows 8j .. 8j+7), 32 for B
-  // (piece j = rows 4j .. 4j+3); wave w issues pieces w + 8r, r < 8.
   // the zero source once, in SGPRs (re-derived per piece it cost an
   // s_load + lgkmcnt(0) wait beside the MFMAs)
   const int8_t* zsrc = g_zero_gemm;
   asm volatile("" : "+s"(zsrc));
   auto issue_r = [&](int st, int r) {  // this wave's piece r of stage st
     const int k0 = st * GK2;
-    const unsigned slot = lds32 + (st & 1) * GSLOT2;
-    {
-      const int pc = wave + 8 * r;
-      if (pc < 32) {
-        const int m = 8 * pc + (lane >> 3), c = (lane & 7) ^ ((m >> 1) & 7), k = k0 + 16 * c;
-        const int8_t* src = (m0 + m < M && k < K) ? A + (size_t)(m0 + m) * K + k : zsrc;
-        glds16_asm(src, slot + pc * 1024);
-      } else {
-        const int q = pc - 32, k = 4 * q + (lane >> 4), b = (lane & 15) ^ (2 * (k & 7)), n = n0 + 16 * b;
-        const int8_t* src = (k0 + k < K && n < N) ? B + (size_t)(k0 + k) * N + n : zsrc;
-        glds16_asm(src, slot + GSLOT2_A + q * 1024);
-      }
+    const unsigned slot = lds32 + (st & 1) * SLOT;
+    const int pc = wave + NW * r;
+    if (pc < PA) {
+      const int m = 8 * pc + (lane >> 3), c = (lane & 7) ^ ((m >> 1) & 7), k = k0 + 16 * c;
+      const int8_t* src = (m0 + m < M && k < K) ? A + (size_t)(m0 + m) * K + k : zsrc;
+      glds16_asm(src, slot + pc * 1024);
+    } else {
+      const int q = pc - PA, k = (1024 / TN) * q + lane / CPR;
+      const int b = (lane % CPR) ^ bswz<TN>(k), n = n0 + 16 * b;
+      const int8_t* src = (k0 + k < K && n < N) ? B + (size_t)(k0 + k) * N + n : zsrc;
+      glds16_asm(src, slot + SA + q * 1024);
     }
   };
-  auto issue = [&](int st) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) issue_r(st, r);
-  };
 
-  v16i acc[4][2];
+  v16i acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = v16i{0};
-  issue(0);
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = v16i{0};
+#pragma unroll
+  for (int r = 0; r < PPW; ++r) issue_r(0, r);
   const int q = (lane & 15) >> 1, p = lane & 1, g = (lane >> 4) & 1;
   for (int s = 0; s < nst; ++s) {
     wait_vm0();  // this wave's pieces of stage s (stage s + 1 is issued below)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // the slot's fragment reads stay below the barrier
-#ifdef DLQ_X_GEMM_OLD
-    if (s + 1 < nst) issue(s + 1);  // into the slot stage s - 1 left
-#endif
-    const int8_t* la = lds + (s & 1) * GSLOT2;
-    const int8_t* lb = la + GSLOT2_A;
+    const int8_t* la = lds + (s & 1) * SLOT;
+    const int8_t* lb = la + SA;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      v4i fa[4], fb[2];
+      v4i fa[MI], fb[NJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = wm * 128 + i * 32 + lr, c = ks * 2 + lh;
+      for (int i = 0; i < MI; ++i) {
+        const int m = (wm * MI + i) * 32 + lr, c = ks * 2 + lh;
         fa[i] = *(const v4i*)(la + m * 128 + 16 * (c ^ ((m >> 1) & 7)));
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int k = ks * 32 + lh * 16 + q, b = wn * 4 + j * 2 + g;
-        const int8_t* a0 = lb + k * 256 + 16 * (b ^ (2 * (k & 7))) + 8 * p;
-        const v2i lo = ds_tr8(a0), hi = ds_tr8(a0 + 8 * 256);
+      for (int j = 0; j < NJ; ++j) {
+        const int k = ks * 32 + lh * 16 + q, b = (wn * NJ + j) * 2 + g;
+        const int8_t* a0 = lb + k * TN + 16 * (b ^ bswz<TN>(k)) + 8 * p;
+        const v2i lo = ds_tr8(a0), hi = ds_tr8(a0 + 8 * TN);
         fb[j] = v4i{lo[0], lo[1], hi[0], hi[1]};
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
-#ifndef DLQ_X_GEMM_OLD
-          // stage s + 1's 8 pieces of this wave (into the slot stage s - 1
-          // left), one after each of k-step 0's MFMAs: the matrix pipe runs
-          // while they issue, instead of idling behind 8 back-to-back DMA
-          // issues after the barrier
-          // (the last stage issues a stage past K: zeros into a slot nobody
-          // reads any more, awaited after the loop)
-          if (ks == 0) {
+          // stage s + 1's pieces of this wave (into the slot stage s - 1
+          // left), one after each of the stage's first PPW MFMAs: the matrix
+          // pipe runs while they issue, instead of idling behind back-to-back
+          // DMA issues after the barrier (the last stage issues a stage past
+          // K: zeros into a slot nobody reads any more, awaited after the loop)
+          if ((ks * MI + i) * NJ + j < PPW) {
             __builtin_amdgcn_sched_barrier(0);
-            issue_r(s + 1, 2 * i + j);
+            issue_r(s + 1, (ks * MI + i) * NJ + j);
             __builtin_amdgcn_sched_barrier(0);
           }
-#endif
         }
     }
   }
-#ifndef DLQ_X_GEMM_OLD
   wait_vm0();  // the past-K stage's pieces land before the workgroup's LDS is released
-#endif
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + lr;
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + (wn * NJ + j) * 32 + lr;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const int m = m0 + (wm * MI + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (m < M && n < N) C[(size_t)m * N + n] = acc[i][j][r];
       }
     }
 }
 
+int num_cus_gemm() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 }  // namespace
 
+// Tile choice for the LDS-DMA kernel (knob "gemm_tile" forces one: 1 =
+// 256 x 256, 2 = 256 x 128, 3 = 128 x 128).  tools/gemm_tiles.py, one box
+// (TOPS for tiles 1 / 2 / 3): 8192^3 1878 / 1736 / 1515; 256 x 50176 x 2304
+// 1491 / 1264 / 1118 and 50176 x 256 x 2304 1513 / 1298 / 1248 (the 256-wide
+// side is read once: 256 x 256 wins although its 196 tiles leave CUs idle);
+// 12544 x 512 x 4608 1009 / 1497 / 1374 (98 tiles of 256 x 256 idle 60 % of
+// the chip); 128 x 200704 x 1152 655 / 585 / 775 (half of a 256-row tile
+// would be padding).
+int gemm_tile_for(int M, int N) {
+  const int forced = g_knob_gemm_tile.load(std::memory_order_relaxed);
+  if (forced >= 1 && forced <= 3) return forced;
+  if (M <= 128) return 3;
+  const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+  if (t256 >= num_cus_gemm() || M <= 256 || N <= 256) return 1;
+  return 2;
+}
+
 hipError_t launch_gemm_s8s8s32(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, hipStream_t s) {
-  const int nbm = (M + GT - 1) / GT, nbn = (N + GT - 1) / GT;
-  const long tiles = (long)nbm * nbn;
-  if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
   if (K % 16 == 0 && N % 16 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0) {
-    hipLaunchKernelGGL(gemm_s8s8s32_k128_kernel, dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M, N, K, nbn);
+    const int cfg = gemm_tile_for(M, N);
+    const int TM = cfg == 3 ? 128 : 256, TN = cfg == 1 ? 256 : 128;
+    const long tiles = (long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+    if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
+    const int nbn = (N + TN - 1) / TN;
+    if (cfg == 1)
+      hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<2, 4, 4, 2, 1>), dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M,
+                         N, K, nbn);
+    else if (cfg == 2)
+      hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<4, 2, 2, 2, 1>), dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M,
+                         N, K, nbn);
+    else
+      hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<2, 2, 2, 2, 2>), dim3((unsigned)tiles), dim3(256), 0, s, A, B, C, M,
+                         N, K, nbn);
   } else {
+    const int nbm = (M + GT - 1) / GT, nbn = (N + GT - 1) / GT;
+    const long tiles = (long)nbm * nbn;
+    if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     const int aligned = K % 16 == 0 && N % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 7) == 0;
     hipLaunchKernelGGL(gemm_s8s8s32_generic_kernel, dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M, N, K, nbn,
                        aligned);

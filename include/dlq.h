@@ -114,7 +114,9 @@ int dlq_pack_conv_weights_s8(const dlq_conv_desc* d, const int8_t* q_oihw, int I
  *                                 workgroup per CU (>0 puts several images in
  *                                 one workgroup);
  *   "head_split" (DLQ_HEAD_SPLIT) 1 = GAP and FC as two launches;
- *   "graph"      (DLQ_GRAPH)      1 = replay the forward as a hipGraph.
+ *   "graph"      (DLQ_GRAPH)      1 = replay the forward as a hipGraph;
+ *   "gemm_tile"  (DLQ_GEMM_TILE)  dlq_gemm_s8s8s32's tile, 0 = by shape,
+ *                                 1 = 256 x 256, 2 = 256 x 128, 3 = 128 x 128.
  * Returns DLQ_ERR_ARG for an unknown name. */
 int dlq_set_knob(const char* name, int value);
 int dlq_get_knob(const char* name, int* value);

@@ -78,6 +78,28 @@ def test_gemm_s8s8s32_reference_layout(gpu, M, N, K):
     assert np.array_equal(Cd.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 528, 2304), (257, 400, 80), (130, 1040, 4608),
+                                   (513, 144, 16)])
+def test_gemm_s8s8s32_every_tile_shape(gpu, knobs, tile, M, N, K):
+    """Each tile of the LDS-DMA kernel (knob gemm_tile: 1 = 256 x 256, 2 = 256 x
+    128, 3 = 128 x 128; by default chosen by shape) on whole tiles, M / N / K
+    tails and K below one stage -- bit-exact with the oracle."""
+    from dlq_amd.lib import lib
+    knobs("gemm_tile", tile)
+    rng = np.random.default_rng(M + 3 * N + 7 * K + tile)
+    A = rand_s8(rng, (M, K), lo=-128)
+    B = rand_s8(rng, (K, N), lo=-128)
+    A.flat[-3:] = -128
+    B.flat[:3] = -128
+    ref = np.empty((M, N), np.int32)
+    O.lib().ora_gemm_s8s8s32(A, B, ref, M, N, K)
+    Cd = torch.full((M, N), 7, dtype=torch.int32, device="cuda")
+    _ok(lib.dlq_gemm_s8s8s32(_p(_cuda(A)), _p(_cuda(B)), _p(Cd), M, N, K, None))
+    torch.cuda.synchronize()
+    assert np.array_equal(Cd.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("M,N,K,a_off,b_off", [(300, 520, 128, 0, 0), (257, 264, 2304, 0, 0), (256, 256, 64, 1, 0),
                                                (300, 520, 128, 0, 8), (200, 512, 256, 16, 24),
                                                (130, 264, 96, 3, 5)])

@@ -1,0 +1,42 @@
+"""dlq_gemm_s8s8s32 TOPS per tile configuration (knob gemm_tile 0 = the
+by-shape choice, 1 = 256 x 256, 2 = 256 x 128, 3 = 128 x 128) on the bench's
+GEMM shapes and the conv-shaped calibration cases: hipEvents over back-to-back
+calls, one process.  python tools/gemm_tiles.py [reps]"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from dlq_amd.lib import check, lib, set_knob  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+dev = torch.device("cuda")
+out = {}
+for (M, N, K) in ((8192, 8192, 8192), (4096, 4096, 4096), (256, 50176, 2304), (12544, 512, 4608),
+                  (50176, 256, 2304), (128, 200704, 1152)):
+    A = torch.randint(-127, 128, (M, K), dtype=torch.int8, device=dev)
+    B = torch.randint(-127, 128, (K, N), dtype=torch.int8, device=dev)
+    C = torch.empty((M, N), dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    res = {}
+    for tile in (0, 1, 2, 3):
+        set_knob("gemm_tile", tile)
+        f = lambda: check(lib.dlq_gemm_s8s8s32(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, st), "gemm")  # noqa
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            f()
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        res[f"tile{tile}"] = {"ms": round(ms, 4), "tops": round(2 * M * N * K / (ms * 1e-3) / 1e12, 1)}
+    set_knob("gemm_tile", 0)
+    out[f"{M}x{N}x{K}"] = res
+    print(f"{M}x{N}x{K}: " + "  ".join(f"{k} {v['tops']:7.1f}" for k, v in res.items()), flush=True)
+    del A, B, C
+print(json.dumps(out))
