@@ -169,23 +169,23 @@ __device__ __forceinline__ void conv3x3i_init(const ConvArgs& a, int8_t* lds) {
 // masking) and its LDS destination a constant offset in the slot (weights,
 // then patch).  With SPS slices per stage, patch piece pc is piece pc % PP of
 // the stage's slice pc / PP, weight piece wp piece wp % WP of slice wp / WP.
-template <int W, int C, int SPS, int NLD>
+template <int W, int C, int SPS, int NLD, int WV>
 struct WideStream {
   using G = IGeo<W, SPS>;
   static constexpr int H = W, NSL = C / ISC, NS = NSL / SPS;
   static constexpr int KP = (G::PPS + NLD - 1) / NLD;  // k < KP: possibly a patch piece
   static constexpr int DPW = (G::NPIECE + NLD - 1) / NLD;  // pieces per loader wave per stage
+  static constexpr int wv = WV;  // this loader wave's rank: every piece's kind is known at compile time
   const ConvArgs& a;
-  int n_ot, it0, nit, nst, wv, lane, iss_li = -1;
+  int n_ot, it0, nit, nst, lane, iss_li = -1;
   unsigned lds32;
   const int8_t* pptr[KP];  // this wave's patch-piece sources for the issuing item's first slice
   const int8_t* wbase;     // the issuing item's weight blocks (wave-uniform)
 
-  __device__ __forceinline__ WideStream(const ConvArgs& a_, int8_t* lds, int lrank) : a(a_) {
+  __device__ __forceinline__ WideStream(const ConvArgs& a_, int8_t* lds) : a(a_) {
     n_ot = a.OCp / G::OT;
     xcd_chunk(n_ot * ((a.P + IL - 1) / IL), it0, nit);
     nst = nit * NS;
-    wv = __builtin_amdgcn_readfirstlane(lrank);
     lane = threadIdx.x & 63;
     lds32 = lds_addr32(lds);
     wbase = a.w;
@@ -246,8 +246,8 @@ struct WideStream {
 
 // RELU (int8, OUT == 0): the output clamp is [0, 127] and the requantisation
 // takes the v_cvt_pk_u8_f32 form (device_common.h quant4_relu).
-template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false, bool RELU = false>
-__device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int mt, int f0, int lrank) {
+template <int W, int C, int OUT, bool RES, int NF, int NLD, int WV, bool F8 = false, bool RELU = false>
+__device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int mt, int f0) {
   constexpr int SPS = sps_of<W, F8>();
   using G = IGeo<W, SPS>;
   constexpr int NS = C / ISC / SPS;  // stages (SPS 32-channel slices each)
@@ -257,7 +257,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   static_assert(DPW <= 2 * KSN, "at most two DMA pieces per k-step");
   static_assert(!F8 || SPS == 1, "fp8: one slice per stage");
   static_assert(SPS <= 2, "the piece -> slice selects below");
-  const bool loader = lrank >= 0;
+  constexpr bool loader = WV < NLD;
   constexpr int STORES = OUT == 0 ? NF : 4 * NF;
   // B fragments two taps ahead for the waves with <= 6 tiles: the younger
   // wave of a SIMD pair runs alone at the end of every stage and, with its
@@ -271,7 +271,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int lr = lane & 31, lh = lane >> 5;
-  WideStream<W, C, SPS, NLD> st(a, lds, lrank);
+  WideStream<W, C, SPS, NLD, WV> st(a, lds);
   const int nst = st.nst;
   auto item_of = [&](int li, int& ot, int& p0) { st.item_of(li, ot, p0); };
   auto issue_piece = [&](int s, int k) { st.issue(s, k); };
@@ -319,7 +319,10 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #ifdef DLQ_X_PRIO
   if (threadIdx.x >= 256) __builtin_amdgcn_s_setprio(1);
 #endif
-  for (int s = 0; s < nst; ++s) {
+  // one stage (s < nst); MORE: a stage follows (its DMA is issued in this
+  // one).  Two instantiations -- every stage but the last, and the last --
+  // so no DMA issue sits behind a runtime branch.
+  auto stage = [&](int s, auto more_c) {
     const int li = s / NS, j = s - li * NS;
     // Stage s has landed once every older VM op is done except the previous
     // item's epilogue stores (issued after this stage's DMA).
@@ -345,7 +348,8 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     }
 #endif
     ISTAMP(1 + 2 * s);
-    const bool more = s + 1 < nst;
+    // (fp8: one instantiation with the runtime test -- two spill its registers)
+    const bool more = decltype(more_c)::value && (!F8 || s + 1 < nst);
     if (more && loader) prep_for(s + 1);
 
     if (j == 0) {
@@ -353,7 +357,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #pragma unroll
       for (int f = 0; f < NF; ++f) acc[f] = Acc{0};
     }
-    const bool dma = more && loader && !DLQ_ABL(a, 2);
+    const bool dma = more && loader && !DLQ_ABL(a, 2);  // compile-time true in library builds
     const int sb = (s & 1) * G::SLOT;
     const int8_t* abase = lds + sb + a_row;
     // this stage's slot: move the tap base registers by one slot (each tap
@@ -522,7 +526,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     }  // int8 MFMA loop
 
     ISTAMP(2 + 2 * s);
-    if (j != NS - 1 || DLQ_ABL(a, 4)) continue;  // probe builds: timing without the epilogue
+    if (j != NS - 1 || DLQ_ABL(a, 4)) return;  // probe builds: timing without the epilogue
     // ---- fused epilogue of the item ----
     if constexpr (OUT == 2) {
 #pragma unroll
@@ -600,6 +604,12 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
         *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
       }
     }
+    };
+  if constexpr (F8) {
+    for (int s = 0; s < nst; ++s) stage(s, std::true_type{});
+  } else {
+    for (int s = 0; s + 1 < nst; ++s) stage(s, std::true_type{});
+    if (nst > 0) stage(nst - 1, std::false_type{});
   }
   ISTAMP(62);
   wait_vm0();
@@ -615,19 +625,28 @@ __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
   const int tid = threadIdx.x;
   int mt, f0, nf;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   wave_tiles<G::MT>(wave, mt, f0, nf);
-  if constexpr (G::MT == 4) {
-    if (nf == 7)
-      conv3x3i_body<W, C, OUT, RES, 7, 8, F8, RELU>(a, lds, mt, f0, wave);
+  // one instantiation per wave: its DMA pieces' kinds and LDS offsets are
+  // compile-time constants (no scalar branches around the issues)
+  auto go = [&](auto wc) {
+    constexpr int w = decltype(wc)::value;
+    if constexpr (G::MT == 4)
+      conv3x3i_body<W, C, OUT, RES, w < 4 ? 7 : 6, INW, w, F8, RELU>(a, lds, mt, f0);
     else
-      conv3x3i_body<W, C, OUT, RES, 6, 8, F8, RELU>(a, lds, mt, f0, wave);
-  } else {
-    if (nf == 4)
-      conv3x3i_body<W, C, OUT, RES, 4, 8, F8, RELU>(a, lds, mt, f0, wave);
-    else
-      conv3x3i_body<W, C, OUT, RES, 3, 8, F8, RELU>(a, lds, mt, f0, wave);
+      conv3x3i_body<W, C, OUT, RES, (w >> 1) == 0 ? 4 : 3, INW, w, F8, RELU>(a, lds, mt, f0);
+  };
+  switch (wave) {
+    case 0: go(std::integral_constant<int, 0>{}); break;
+    case 1: go(std::integral_constant<int, 1>{}); break;
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 3: go(std::integral_constant<int, 3>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    case 5: go(std::integral_constant<int, 5>{}); break;
+    case 6: go(std::integral_constant<int, 6>{}); break;
+    default: go(std::integral_constant<int, 7>{}); break;
   }
+  (void)nf;
 }
 
 int num_cus_i() {

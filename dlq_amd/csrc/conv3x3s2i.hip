@@ -151,7 +151,9 @@ __device__ __forceinline__ int perm_at(int slot) {
 // RELU (int8, OUT == 0): conv1's clamp is [0, 127], requantised in the
 // v_cvt_pk_u8_f32 form (device_common.h quant4_relu); the downsample keeps
 // the signed clamp.
-template <int OW, int C, int OUT, bool DS, int NF, bool F8, bool RW, bool RELU = false>
+// WV: this wave's index (compile-time, so each DMA piece's kind and LDS
+// offset are constants: no scalar branches around the issues).
+template <int OW, int C, int OUT, bool DS, int NF, int WV, bool F8, bool RW, bool RELU = false>
 __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, const float* be_ds,
                                          int8_t* y_ds, int8_t* lds, int mt, int f0) {
   using G = JGeo<OW, DS, RW ? C / JSC : 0>;
@@ -160,7 +162,8 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
   static_assert(DPW <= 18, "at most two DMA pieces per tap");
   constexpr int STORES = OUT == 0 ? (DS ? 2 * NF : NF) : 4 * NF;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr int wave = WV;
   const int lr = lane & 31, lh = lane >> 5;
   const int n_ot = a.OCp / JOT;
   const int NI = n_ot * ((a.P + JL - 1) / JL);
@@ -182,7 +185,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
   // in the slot.
   constexpr int KP = (G::PP + JNW - 1) / JNW;  // k < KP: possibly a patch piece
   constexpr int WCP = G::WB / 1024;            // conv weight pieces (then ds pieces)
-  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  constexpr int wv = WV;
   const int8_t* pptr[KP];
   const int8_t* wb_c = a.w;   // the issuing item's conv / downsample weight blocks (wave-uniform)
   const int8_t* wb_d = w_ds;
@@ -295,7 +298,10 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
 #ifdef DLQ_X_PRIO
   if (threadIdx.x >= 256) __builtin_amdgcn_s_setprio(1);
 #endif
-  for (int s = 0; s < nst; ++s) {
+  // one stage (s < nst); MORE: a stage follows (its DMA is issued in this
+  // one).  int8: every stage but the last, and the last, as two
+  // instantiations, so no DMA issue sits behind a runtime branch.
+  auto stage = [&](int s, auto more_c) {
     const int li = s / NS, j = s - li * NS;
     if (s == 0) JSTAMP(58);
     if (j == 0 && s > 0)
@@ -330,7 +336,8 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     }
 #endif
     JSTAMP(1 + 2 * s);
-    const bool more = s + 1 < nst;
+    // (fp8: one instantiation with the runtime test -- two spill its registers)
+    const bool more = decltype(more_c)::value && (!F8 || s + 1 < nst);
     if (more) prep_for(s + 1);
     if (j == 0) {
       item_of(li, cur_ot, cur_p0);
@@ -452,7 +459,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     }  // int8 MFMA loop
 
     JSTAMP(2 + 2 * s);
-    if (j != NS - 1 || DLQ_ABL(a, 4)) continue;  // probe builds: timing without the epilogues
+    if (j != NS - 1 || DLQ_ABL(a, 4)) return;  // probe builds: timing without the epilogues
     // ---- fused epilogues of the item ----
     if constexpr (OUT == 2) {
 #pragma unroll
@@ -517,6 +524,12 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
         if (!DLQ_ABL(a, 8)) epi(accd, 2 * OC * 4, LO, y_ds, std::integral_constant<bool, false>{}, DLQ_ABL(a, 16));
       }
     }
+    };
+  if constexpr (F8) {
+    for (int s = 0; s < nst; ++s) stage(s, std::true_type{});
+  } else {
+    for (int s = 0; s + 1 < nst; ++s) stage(s, std::true_type{});
+    if (nst > 0) stage(nst - 1, std::false_type{});
   }
   JSTAMP(62);
   wait_vm0();
@@ -532,11 +545,21 @@ __global__ __launch_bounds__(JNW * 64, 1) void conv3x3s2i_kernel(ConvArgs a, con
   constexpr int LDS_TOTAL = G::OFF_AB + (DS ? 4 : 2) * OC * 4;
   static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
-  const int wave = threadIdx.x >> 6;
-  if (wave < 4)
-    s2i_body<OW, C, OUT, DS, 4, F8, RW, RELU>(a, w_ds, al_ds, be_ds, y_ds, lds, wave & 3, 0);
-  else
-    s2i_body<OW, C, OUT, DS, 3, F8, RW, RELU>(a, w_ds, al_ds, be_ds, y_ds, lds, wave & 3, 4);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  auto go = [&](auto wc) {  // one instantiation per wave (see s2i_body)
+    constexpr int w = decltype(wc)::value;
+    s2i_body<OW, C, OUT, DS, w < 4 ? 4 : 3, w, F8, RW, RELU>(a, w_ds, al_ds, be_ds, y_ds, lds, w & 3, w < 4 ? 0 : 4);
+  };
+  switch (wave) {
+    case 0: go(std::integral_constant<int, 0>{}); break;
+    case 1: go(std::integral_constant<int, 1>{}); break;
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 3: go(std::integral_constant<int, 3>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    case 5: go(std::integral_constant<int, 5>{}); break;
+    case 6: go(std::integral_constant<int, 6>{}); break;
+    default: go(std::integral_constant<int, 7>{}); break;
+  }
 }
 
 int num_cus_s2i() {
