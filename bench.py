@@ -335,7 +335,7 @@ def extra_configs(dev):
             st = torch.cuda.current_stream().cuda_stream
             fn = lambda: check(lib.dlq_gemm_s8s8s32(A.data_ptr(), Bm.data_ptr(), Cm.data_ptr(), M, N, K, st),  # noqa: E731
                                "gemm")
-            ms = timed_cuda(fn, 10)
+            ms = timed_cuda(fn, 20, warmup=10)
             tops = 2.0 * M * N * K / (ms * 1e-3) / 1e12
             res[f"{M}x{N}x{K}"] = {"ms": round(ms, 4), "tops": round(tops, 1), "frac": round(tops / PEAK_I8_TOPS, 4)}
             del A, Bm, Cm
