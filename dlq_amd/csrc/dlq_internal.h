@@ -103,6 +103,8 @@ hipError_t launch_gap_fc(const int8_t* x, int N, int C, int HW, float k, const i
                          const float* alpha, const float* beta, float* y, hipStream_t s);  // C == 512, HW <= 56
 // dlq_gemm_s8s8s32 (gemm.hip): row-major int8 A[M][K] . B[K][N] -> int32 C.
 hipError_t launch_gemm_s8s8s32(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, hipStream_t s);
+// dlq_gemm_s8s8s32_nt (gemm.hip): the same with B supplied as Bt[N][K].
+hipError_t launch_gemm_s8s8s32_nt(const int8_t* A, const int8_t* Bt, int32_t* C, int M, int N, int K, hipStream_t s);
 hipError_t launch_im2col_nchw(const int8_t* x, int N, int C, int H, int W, int kH, int kW, int sH,
                               int sW, int pH, int pW, int8_t* col, hipStream_t s);
 

@@ -42,6 +42,9 @@ __device__ __forceinline__ unsigned ld_bytes(const int8_t* p, int avail) {  // u
   return v;
 }
 
+// BT: B is supplied transposed, Bt[N][K] (K-contiguous rows, loaded and
+// staged exactly as A's rows: no register transpose).
+template <bool BT>
 __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_generic_kernel(const int8_t* __restrict__ A,
                                                              const int8_t* __restrict__ B, int32_t* __restrict__ C,
                                                              int M, int N, int K, int nbn, int aligned) {
@@ -60,12 +63,19 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_generic_kernel(const int8
   // each load has two stages of MFMAs to land before its LDS write.
   v4i ra[2][2];
   unsigned rb[2][4][2];
+  v4i rbt[2][2];  // BT: rows n0 + a_row (+128), chunk a_ch
 
   auto gload = [&](int k0, int set) {
     if (full_mn && k0 + GK <= K) {
 #pragma unroll
       for (int p = 0; p < 2; ++p)
         ra[set][p] = *(const v4i*)(A + (size_t)(m0 + a_row + 128 * p) * K + k0 + a_ch * 16);
+      if constexpr (BT) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          rbt[set][p] = *(const v4i*)(B + (size_t)(n0 + a_row + 128 * p) * K + k0 + a_ch * 16);
+        return;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const uint2 v = *(const uint2*)(B + (size_t)(k0 + 4 * b_rq + r) * N + n0 + 8 * b_cg);
@@ -81,6 +91,16 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_generic_kernel(const int8
 #pragma unroll
       for (int w = 0; w < 4; ++w) ra[set][p][w] = (int)(m < M ? ld_bytes(src + 4 * w, K - k - 4 * w) : 0u);
     }
+    if constexpr (BT) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int n = n0 + a_row + 128 * p, k = k0 + a_ch * 16;
+        const int8_t* src = B + (size_t)n * K + k;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) rbt[set][p][w] = (int)(n < N ? ld_bytes(src + 4 * w, K - k - 4 * w) : 0u);
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int k = k0 + 4 * b_rq + r, n = n0 + 8 * b_cg;
@@ -94,6 +114,11 @@ __global__ __launch_bounds__(512, 1) void gemm_s8s8s32_generic_kernel(const int8
     int8_t* lb = la + GT * GP;
 #pragma unroll
     for (int p = 0; p < 2; ++p) *(v4i*)(la + (a_row + 128 * p) * GP + a_ch * 16) = ra[set][p];
+    if constexpr (BT) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) *(v4i*)(lb + (a_row + 128 * p) * GP + a_ch * 16) = rbt[set][p];
+      return;
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {  // 4 x 4 byte transpose: rows k..k+3 -> column dwords
       const unsigned t0 = __builtin_amdgcn_perm(rb[set][1][h], rb[set][0][h], 0x05010400u);
@@ -201,7 +226,10 @@ __device__ __forceinline__ int bswz(int k) {
   return TN == 256 ? 2 * (k & 7) : 2 * ((k >> 1) & 3);
 }
 
-template <int WM, int WN, int MI, int NJ, int WPS>
+// BT: B supplied transposed (Bt[N][K]): its tile is staged and read exactly
+// as A's (rows of 128 K bytes, chunk c at n*128 + 16*(c ^ ((n >> 1) & 7))),
+// one ds_read_b128 per B fragment instead of two ds_read_b64_tr_b8.
+template <int WM, int WN, int MI, int NJ, int WPS, bool BT = false>
 __global__ __launch_bounds__(WM * WN * 64, WPS) void gemm_s8s8s32_k128_kernel(const int8_t* __restrict__ A,
                                                                              const int8_t* __restrict__ B,
                                                                              int32_t* __restrict__ C, int M, int N,
@@ -233,6 +261,10 @@ __global__ __launch_bounds__(WM * WN * 64, WPS) void gemm_s8s8s32_k128_kernel(co
       const int m = 8 * pc + (lane >> 3), c = (lane & 7) ^ ((m >> 1) & 7), k = k0 + 16 * c;
       const int8_t* src = (m0 + m < M && k < K) ? A + (size_t)(m0 + m) * K + k : zsrc;
       glds16_asm(src, slot + pc * 1024);
+    } else if constexpr (BT) {
+      const int q = pc - PA, n = 8 * q + (lane >> 3), c = (lane & 7) ^ ((n >> 1) & 7), k = k0 + 16 * c;
+      const int8_t* src = (n0 + n < N && k < K) ? B + (size_t)(n0 + n) * K + k : zsrc;
+      glds16_asm(src, slot + SA + q * 1024);
     } else {
       const int q = pc - PA, k = (1024 / TN) * q + lane / CPR;
       const int b = (lane % CPR) ^ bswz<TN>(k), n = n0 + 16 * b;
@@ -265,10 +297,15 @@ __global__ __launch_bounds__(WM * WN * 64, WPS) void gemm_s8s8s32_k128_kernel(co
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int k = ks * 32 + lh * 16 + q, b = (wn * NJ + j) * 2 + g;
-        const int8_t* a0 = lb + k * TN + 16 * (b ^ bswz<TN>(k)) + 8 * p;
-        const v2i lo = ds_tr8(a0), hi = ds_tr8(a0 + 8 * TN);
-        fb[j] = v4i{lo[0], lo[1], hi[0], hi[1]};
+        if constexpr (BT) {
+          const int n = (wn * NJ + j) * 32 + lr, c = ks * 2 + lh;
+          fb[j] = *(const v4i*)(lb + n * 128 + 16 * (c ^ ((n >> 1) & 7)));
+        } else {
+          const int k = ks * 32 + lh * 16 + q, b = (wn * NJ + j) * 2 + g;
+          const int8_t* a0 = lb + k * TN + 16 * (b ^ bswz<TN>(k)) + 8 * p;
+          const v2i lo = ds_tr8(a0), hi = ds_tr8(a0 + 8 * TN);
+          fb[j] = v4i{lo[0], lo[1], hi[0], hi[1]};
+        }
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -332,31 +369,46 @@ int gemm_tile_for(int M, int N) {
   return 2;
 }
 
-hipError_t launch_gemm_s8s8s32(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, hipStream_t s) {
-  if (K % 16 == 0 && N % 16 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0) {
+namespace {
+template <bool BT>
+hipError_t launch_gemm(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, hipStream_t s) {
+  // NN: K, N multiples of 16 (B rows are 16-byte chunks of N); NT: K alone
+  const bool dma = K % 16 == 0 && (BT || N % 16 == 0) && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0;
+  if (dma) {
     const int cfg = gemm_tile_for(M, N);
     const int TM = cfg == 3 ? 128 : 256, TN = cfg == 1 ? 256 : 128;
     const long tiles = (long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     const int nbn = (N + TN - 1) / TN;
     if (cfg == 1)
-      hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<2, 4, 4, 2, 1>), dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M,
-                         N, K, nbn);
+      hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<2, 4, 4, 2, 1, BT>), dim3((unsigned)tiles), dim3(512), 0, s, A, B, C,
+                         M, N, K, nbn);
     else if (cfg == 2)
-      hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<4, 2, 2, 2, 1>), dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M,
-                         N, K, nbn);
+      hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<4, 2, 2, 2, 1, BT>), dim3((unsigned)tiles), dim3(512), 0, s, A, B, C,
+                         M, N, K, nbn);
     else
-      hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<2, 2, 2, 2, 2>), dim3((unsigned)tiles), dim3(256), 0, s, A, B, C, M,
-                         N, K, nbn);
+      hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<2, 2, 2, 2, 2, BT>), dim3((unsigned)tiles), dim3(256), 0, s, A, B, C,
+                         M, N, K, nbn);
   } else {
     const int nbm = (M + GT - 1) / GT, nbn = (N + GT - 1) / GT;
     const long tiles = (long)nbm * nbn;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
-    const int aligned = K % 16 == 0 && N % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 7) == 0;
-    hipLaunchKernelGGL(gemm_s8s8s32_generic_kernel, dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M, N, K, nbn,
+    const int aligned = BT ? K % 16 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0
+                           : K % 16 == 0 && N % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 7) == 0;
+    hipLaunchKernelGGL(gemm_s8s8s32_generic_kernel<BT>, dim3((unsigned)tiles), dim3(512), 0, s, A, B, C, M, N, K, nbn,
                        aligned);
   }
   return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_gemm_s8s8s32(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, hipStream_t s) {
+  return launch_gemm<false>(A, B, C, M, N, K, s);
+}
+
+// B supplied transposed: C[M][N] = A[M][K] . Bt[N][K]^T.
+hipError_t launch_gemm_s8s8s32_nt(const int8_t* A, const int8_t* Bt, int32_t* C, int M, int N, int K, hipStream_t s) {
+  return launch_gemm<true>(A, Bt, C, M, N, K, s);
 }
 
 }  // namespace dlq

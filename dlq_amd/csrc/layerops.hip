@@ -165,6 +165,15 @@ int dlq_gemm_s8s8s32(const int8_t* A, const int8_t* B, int32_t* C, int M, int N,
   return status(launch_gemm_s8s8s32(A, B, C, M, N, K, (hipStream_t)stream), "gemm_s8s8s32");
 }
 
+int dlq_gemm_s8s8s32_nt(const int8_t* A, const int8_t* Bt, int32_t* C, int M, int N, int K, void* stream) {
+  if (M < 0 || N < 0 || K < 0) return fail(DLQ_ERR_ARG, "gemm_s8s8s32_nt: negative size");
+  if (M == 0 || N == 0) return DLQ_OK;
+  if (!A || !Bt || !C) return fail(DLQ_ERR_ARG, "gemm_s8s8s32_nt: null pointer");
+  if ((long long)M * K >= (1LL << 31) || (long long)K * N >= (1LL << 31) || (long long)M * N >= (1LL << 31))
+    return fail(DLQ_ERR_ARG, "gemm_s8s8s32_nt: operand exceeds 2^31 elements");
+  return status(launch_gemm_s8s8s32_nt(A, Bt, C, M, N, K, (hipStream_t)stream), "gemm_s8s8s32_nt");
+}
+
 size_t dlq_conv2d_nchw_workspace_bytes(int N, int IC, int H, int W, int OC, int kH, int kW, int sH, int sW, int pH,
                                        int pW) {
   const int Cs = stored_c(IC, kH, kW);

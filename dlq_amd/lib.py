@@ -56,6 +56,7 @@ _SIGS = {
     "dlq_finalize": ([], _i),
     "dlq_quantize_f32_s8": ([_vp, _sz, _f, _vp, _vp], _i),
     "dlq_gemm_s8s8s32": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
+    "dlq_gemm_s8s8s32_nt": ([_vp, _vp, _vp, _i, _i, _i, _vp], _i),
     "dlq_conv2d_nchw_workspace_bytes": ([_i] * 11, _sz),
     "dlq_conv2d_nchw_s8": ([_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp,
                             _sz, _vp, C.POINTER(_i), C.POINTER(_i)], _i),

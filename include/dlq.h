@@ -131,6 +131,13 @@ int dlq_quantize_f32_s8(const float* x, size_t n, float inv_s, int8_t* q, void* 
 /* sgemm_tiled (RK/kernels/sgemm_tiled.cu:5-46) on int8: C[M][N] (int32) =
  * A[M][K] . B[K][N], all row-major, any M, N, K. */
 int dlq_gemm_s8s8s32(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, void* stream);
+/* The same contraction with B supplied transposed, Bt[N][K] (each output
+ * column's K bytes contiguous, as the MFMA's B operand wants): C[M][N] =
+ * A[M][K] . Bt^T.  New (the reference's sgemm_tiled is NN only); for callers
+ * that hold the im2col panel K-contiguous, or weights as the right operand.
+ * Any M, N, K; the LDS-DMA kernel needs only K % 16 == 0 and 16-byte aligned
+ * A / Bt.  int32 results identical to dlq_gemm_s8s8s32 on B = Bt^T. */
+int dlq_gemm_s8s8s32_nt(const int8_t* A, const int8_t* Bt, int32_t* C, int M, int N, int K, void* stream);
 /* conv2d_nchw_im2col_gemm (RK/runtime/infer_e2e.cu:102-136; + bn_launch
  * :83-97 + relu) on int8: x[N][IC][H][W], w_oihw[OC][IC][kH][kW] (int8,
  * packed and uploaded per call like the reference's per-call weight copy),

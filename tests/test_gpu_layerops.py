@@ -128,6 +128,35 @@ def test_gemm_s8s8s32_kernel_selection(gpu, M, N, K, a_off, b_off):
     assert np.array_equal(Cd.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K,a_off,b_off", [(256, 256, 128, 0, 0), (300, 521, 2304, 0, 0), (257, 400, 80, 0, 0),
+                                               (130, 1040, 4608, 0, 0), (513, 7, 16, 0, 0), (100, 77, 61, 0, 0),
+                                               (33, 65, 1, 0, 0), (300, 520, 128, 0, 8), (130, 264, 96, 3, 5)])
+def test_gemm_s8s8s32_nt(gpu, knobs, tile, M, N, K, a_off, b_off):
+    """dlq_gemm_s8s8s32_nt (B supplied as Bt[N][K]): every LDS-DMA tile on
+    whole tiles, M / N / K tails and any N (no N % 16 condition), and the
+    register-staged kernel for K % 16 != 0 or unaligned bases (a_off /
+    b_off), bit-exact with the oracle's NN GEMM of B = Bt^T."""
+    from dlq_amd.lib import lib
+    knobs("gemm_tile", tile)
+    rng = np.random.default_rng(M + 5 * N + 11 * K + tile + a_off)
+    A = rand_s8(rng, (M, K), lo=-128)
+    Bt = rand_s8(rng, (N, K), lo=-128)
+    A.flat[:3] = -128
+    Bt.flat[-3:] = -128
+    B = np.ascontiguousarray(Bt.T)
+    ref = np.empty((M, N), np.int32)
+    O.lib().ora_gemm_s8s8s32(A, B, ref, M, N, K)
+    abuf = torch.zeros(M * K + 64, dtype=torch.int8, device="cuda")
+    bbuf = torch.zeros(K * N + 64, dtype=torch.int8, device="cuda")
+    abuf[a_off:a_off + M * K] = torch.from_numpy(A.reshape(-1)).cuda()
+    bbuf[b_off:b_off + K * N] = torch.from_numpy(Bt.reshape(-1)).cuda()
+    Cd = torch.full((M, N), 7, dtype=torch.int32, device="cuda")
+    _ok(lib.dlq_gemm_s8s8s32_nt(abuf.data_ptr() + a_off, bbuf.data_ptr() + b_off, _p(Cd), M, N, K, None))
+    torch.cuda.synchronize()
+    assert np.array_equal(Cd.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("IC,OC,k,s,p,H,N", [(3, 64, 7, 2, 3, 224, 1), (64, 64, 3, 1, 1, 56, 2),
                                              (64, 128, 1, 2, 0, 56, 2), (128, 128, 3, 1, 1, 28, 3),
                                              (256, 512, 3, 2, 1, 14, 2)])

@@ -1,7 +1,8 @@
-"""dlq_gemm_s8s8s32 TOPS per tile configuration (knob gemm_tile 0 = the
-by-shape choice, 1 = 256 x 256, 2 = 256 x 128, 3 = 128 x 128) on the bench's
-GEMM shapes and the conv-shaped calibration cases: hipEvents over back-to-back
-calls, one process.  python tools/gemm_tiles.py [reps]"""
+"""dlq_gemm_s8s8s32 (NN: B[K][N]) and dlq_gemm_s8s8s32_nt (NT: Bt[N][K]) TOPS
+per tile configuration (knob gemm_tile 0 = the by-shape choice, 1 = 256 x 256,
+2 = 256 x 128, 3 = 128 x 128) on the bench's GEMM shapes and the conv-shaped
+calibration cases: hipEvents over back-to-back calls, one process.
+python tools/gemm_tiles.py [reps]"""
 import json
 import os
 import sys
@@ -21,9 +22,10 @@ for (M, N, K) in ((8192, 8192, 8192), (4096, 4096, 4096), (256, 50176, 2304), (1
     C = torch.empty((M, N), dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream().cuda_stream
     res = {}
-    for tile in (0, 1, 2, 3):
+    for lay, tile in [(lay, t) for lay in ("nn", "nt") for t in (0, 1, 2, 3)]:
         set_knob("gemm_tile", tile)
-        f = lambda: check(lib.dlq_gemm_s8s8s32(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, st), "gemm")  # noqa
+        fn = lib.dlq_gemm_s8s8s32 if lay == "nn" else lib.dlq_gemm_s8s8s32_nt  # B's bytes reused as Bt[N][K]
+        f = lambda: check(fn(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, st), "gemm")  # noqa
         for _ in range(3):
             f()
         torch.cuda.synchronize()
@@ -34,7 +36,7 @@ for (M, N, K) in ((8192, 8192, 8192), (4096, 4096, 4096), (256, 50176, 2304), (1
         e1.record()
         e1.synchronize()
         ms = e0.elapsed_time(e1) / reps
-        res[f"tile{tile}"] = {"ms": round(ms, 4), "tops": round(2 * M * N * K / (ms * 1e-3) / 1e12, 1)}
+        res[f"{lay}{tile}"] = {"ms": round(ms, 4), "tops": round(2 * M * N * K / (ms * 1e-3) / 1e12, 1)}
     set_knob("gemm_tile", 0)
     out[f"{M}x{N}x{K}"] = res
     print(f"{M}x{N}x{K}: " + "  ".join(f"{k} {v['tops']:7.1f}" for k, v in res.items()), flush=True)
