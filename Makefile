@@ -11,7 +11,7 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -
 SRC = dlq_amd/csrc/kernels.hip dlq_amd/csrc/conv3x3.hip dlq_amd/csrc/conv3x3i.hip dlq_amd/csrc/conv3x3s2i.hip dlq_amd/csrc/block_l1.hip dlq_amd/csrc/stem.hip dlq_amd/csrc/head.hip dlq_amd/csrc/layerops.hip dlq_amd/csrc/gemm.hip dlq_amd/csrc/preproc.hip dlq_amd/csrc/fp8.hip dlq_amd/csrc/ref_f32.hip dlq_amd/csrc/capi.cpp dlq_amd/csrc/resnet18.cpp dlq_amd/csrc/mlp.cpp dlq_amd/csrc/wpack.cpp
 HDR = include/dlq.h dlq_amd/csrc/dlq_internal.h dlq_amd/csrc/device_common.h
 
-all: dlq_amd/libdlq.so bin/dlq_e2e bin/dlq_step oracle
+all: dlq_amd/libdlq.so bin/dlq_e2e bin/dlq_step tools/check/libplancap.so oracle
 
 # the layer1 block interleaves its epilogue FMAs with MFMAs: keep them scalar
 build/block_l1.o: HIPFLAGS += -fno-slp-vectorize
@@ -35,11 +35,16 @@ bin/dlq_step: dlq_amd/csrc/main_step.cpp dlq_amd/libdlq.so include/dlq.h
 	@mkdir -p bin
 	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -Ldlq_amd -ldlq -Wl,-rpath,'$$ORIGIN/../dlq_amd'
 
+# test infrastructure: the convs' LDS-DMA plans recorded by the kernels
+# themselves (tests/test_gpu_dma_plan.py)
+tools/check/libplancap.so: tools/check/plan_capture.hip dlq_amd/csrc/conv3x3i.hip dlq_amd/csrc/conv3x3s2i.hip $(HDR)
+	$(HIPCC) $(HIPFLAGS) -shared -I dlq_amd/csrc -o $@ $<
+
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build bin dlq_amd/libdlq.so
+	rm -rf build bin dlq_amd/libdlq.so tools/check/libplancap.so
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

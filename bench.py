@@ -333,18 +333,47 @@ def extra_configs(dev):
             Bm = torch.randint(-127, 128, (K, N), dtype=torch.int8, device=dev)
             Cm = torch.empty((M, N), dtype=torch.int32, device=dev)
             st = torch.cuda.current_stream().cuda_stream
-            fn = lambda: check(lib.dlq_gemm_s8s8s32(A.data_ptr(), Bm.data_ptr(), Cm.data_ptr(), M, N, K, st),  # noqa: E731
-                               "gemm")
-            ms = timed_cuda(fn, 20, warmup=10)
-            tops = 2.0 * M * N * K / (ms * 1e-3) / 1e12
-            res[f"{M}x{N}x{K}"] = {"ms": round(ms, 4), "tops": round(tops, 1), "frac": round(tops / PEAK_I8_TOPS, 4)}
+            for lay, gemm in (("", lib.dlq_gemm_s8s8s32), ("_nt", lib.dlq_gemm_s8s8s32_nt)):
+                # NT: the same bytes read as Bt[N][K] (dlq_gemm_s8s8s32_nt)
+                fn = lambda: check(gemm(A.data_ptr(), Bm.data_ptr(), Cm.data_ptr(), M, N, K, st), "gemm")  # noqa: E731
+                ms = timed_cuda(fn, 20, warmup=10)
+                tops = 2.0 * M * N * K / (ms * 1e-3) / 1e12
+                res[f"{M}x{N}x{K}{lay}"] = {"ms": round(ms, 4), "tops": round(tops, 1),
+                                            "frac": round(tops / PEAK_I8_TOPS, 4)}
             del A, Bm, Cm
-        out["gemm_s8s8s32"] = {"kernel": "gemm_s8s8s32_k128_kernel (gemm.hip), tile chosen by shape",
+        out["gemm_s8s8s32"] = {"kernel": "gemm_s8s8s32_k128_kernel (gemm.hip), tile chosen by shape; "
+                                         "*_nt = dlq_gemm_s8s8s32_nt (B as Bt[N][K])",
                                "peak_tops": round(PEAK_I8_TOPS, 1),
                                "shapes": "8192^3; the layer-conv shapes OC x pixels x K (256 x 50176 x 2304) and "
                                          "pixels x OC x K (12544 x 512 x 4608)", **res}
     except Exception as e:
         out["gemm error"] = repr(e)
+    # the standalone quantise / dequant passes of the per-layer ABI: HBM GB/s
+    # (algorithmic bytes: fp32 in + int8 out; int32 in + fp32 out)
+    try:
+        st = torch.cuda.current_stream().cuda_stream
+        n = 256 * 3 * 224 * 224
+        xq = torch.randn(n, device=dev)
+        qq = torch.empty(n, dtype=torch.int8, device=dev)
+        ms_q = timed_cuda(lambda: check(lib.dlq_quantize_f32_s8(xq.data_ptr(), n, 50.0, qq.data_ptr(), st),  # noqa: E731
+                                        "quantize"), 20, warmup=5)
+        NB, CC, HW = 256, 64, 56 * 56
+        acc = torch.randint(-(1 << 20), 1 << 20, (NB, CC, HW), dtype=torch.int32, device=dev)
+        sc = torch.rand(CC, device=dev)
+        yd = torch.empty((NB, CC, HW), dtype=torch.float32, device=dev)
+        ms_d = timed_cuda(lambda: check(lib.dlq_dequant_s32_f32(acc.data_ptr(), NB, CC, HW, sc.data_ptr(),  # noqa: E731
+                                                                yd.data_ptr(), st), "dequant"), 20, warmup=5)
+        out["quant_dequant_hbm"] = {
+            "quantize_f32_s8": {"elements": n, "bytes": 5 * n, "ms": round(ms_q, 4),
+                                "gb_s": round(5 * n / (ms_q * 1e-3) / 1e9, 1)},
+            "dequant_s32_f32": {"elements": NB * CC * HW, "bytes": 8 * NB * CC * HW, "ms": round(ms_d, 4),
+                                "gb_s": round(8 * NB * CC * HW / (ms_d * 1e-3) / 1e9, 1)},
+            "peak_gb_s": 8000.0,
+            "kernels": "quantize_f32_s8_v4_kernel / dequant_s32_f32_v4_kernel (layerops.hip)",
+            "shapes": "quantize: the B=256 fp32 input tensor; dequant: int32 [256][64][56x56] (layer1-sized)"}
+        del xq, qq, acc, yd
+    except Exception as e:
+        out["quant_dequant error"] = repr(e)
     # configs[4]: fp8 (e4m3) activations + per-channel e4m3 weights, B = 256
     try:
         sd = resnet18_state_dict(SEED)

@@ -206,8 +206,39 @@ __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" :
 // treats as a possible FLAT-LDS access: every later ds_read wait then becomes
 // lgkmcnt(0), draining the fragment prefetch.  Completion must be covered by
 // the caller's explicit vmcnt counts + barrier.
+#ifdef DLQ_PLAN_CAPTURE
+// Plan-capture builds (tools/check/plan_capture.hip, never libdlq.so): every
+// LDS-DMA piece is recorded instead of issued -- its M0 LDS address and the
+// 64 lanes' source addresses, in issue order per (workgroup, wave) -- so the
+// host checker (tools/check/dma_plan.py) is compared with the compiled
+// kernels' own plans (tests/test_gpu_dma_plan.py).
+struct PlanPiece {
+  unsigned long long src[64];
+  unsigned lds, pad[3];
+};
+__device__ PlanPiece* g_cap_buf;
+__device__ unsigned* g_cap_cnt;
+__device__ unsigned g_cap_max;
+__device__ __forceinline__ void plan_capture(const void* gsrc, unsigned lds_addr) {
+  const int lane = threadIdx.x & 63;
+  const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  unsigned i = 0;
+  if (lane == 0) i = atomicAdd(&g_cap_cnt[w], 1u);
+  i = (unsigned)__shfl((int)i, 0);
+  if (i < g_cap_max) {
+    PlanPiece* r = g_cap_buf + (size_t)w * g_cap_max + i;
+    r->src[lane] = (unsigned long long)(uintptr_t)gsrc;
+    if (lane == 0) r->lds = lds_addr;
+  }
+}
+#endif
+
 __device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_addr) {
   const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
+#ifdef DLQ_PLAN_CAPTURE
+  plan_capture(gsrc, m0);
+  return;
+#endif
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "{m0}"(m0) : "memory");
 }
 
@@ -216,6 +247,10 @@ __device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_addr) 
 // compiler in 64-bit pointer arithmetic from uniform values).
 __device__ __forceinline__ void glds16_saddr(const void* base, unsigned voff, unsigned lds_addr) {
   const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
+#ifdef DLQ_PLAN_CAPTURE
+  plan_capture((const char*)base + voff, m0);
+  return;
+#endif
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(base), "{m0}"(m0) : "memory");
 }
 

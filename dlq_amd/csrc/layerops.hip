@@ -21,6 +21,17 @@
 namespace dlq {
 namespace {
 
+int num_cus_layerops() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 inline unsigned grid1(size_t total, int per = 256) {
   size_t g = (total + per - 1) / per;
   if (g > 256 * 64) g = 256 * 64;
@@ -31,6 +42,55 @@ __global__ void quantize_f32_s8_kernel(const float* __restrict__ x, size_t n, fl
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     q[i] = (int8_t)sat_rne(x[i] * inv_s);
 }
+
+// The HBM-streaming forms of the standalone quantise / dequant passes (x, q /
+// acc, y 16-byte aligned; the scalar kernels above take the rest and the
+// tails).  Grid = 8 workgroups of 256 per CU, each thread 4 independent
+// 16-byte loads in flight per iteration (coalesced: consecutive lanes,
+// consecutive 16-byte units), and the same per-element IEEE ops as the scalar
+// kernels (sat_rne(x * inv_s); float(acc) * scale[c]): bit-identical.
+constexpr int QV_UNROLL = 4;
+__global__ __launch_bounds__(256) void quantize_f32_s8_v4_kernel(const float4* __restrict__ x, size_t n4, float inv_s,
+                                                                 unsigned* __restrict__ q) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  auto q4 = [&](const float4 v) -> unsigned {
+    return ((unsigned)sat_rne(v.x * inv_s) & 0xffu) | (((unsigned)sat_rne(v.y * inv_s) & 0xffu) << 8) |
+           (((unsigned)sat_rne(v.z * inv_s) & 0xffu) << 16) | (((unsigned)sat_rne(v.w * inv_s) & 0xffu) << 24);
+  };
+  for (; i + (QV_UNROLL - 1) * stride < n4; i += QV_UNROLL * stride) {
+    float4 v[QV_UNROLL];
+#pragma unroll
+    for (int u = 0; u < QV_UNROLL; ++u) v[u] = x[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < QV_UNROLL; ++u) q[i + u * stride] = q4(v[u]);
+  }
+  for (; i < n4; i += stride) q[i] = q4(x[i]);
+}
+
+// HW % 4 == 0: a 16-byte group never crosses a channel row.  IDX: 32-bit
+// index arithmetic when the element count allows it.
+template <typename IDX>
+__global__ __launch_bounds__(256) void dequant_s32_f32_v4_kernel(const int4* __restrict__ acc, IDX n4, IDX hw4, int C,
+                                                                 const float* __restrict__ scale,
+                                                                 float4* __restrict__ y) {
+  const IDX stride = (IDX)gridDim.x * blockDim.x;
+  IDX i = (IDX)blockIdx.x * blockDim.x + threadIdx.x;
+  auto dq = [&](const int4 a, IDX j) -> float4 {
+    const float s = scale[(int)((j / hw4) % (IDX)C)];
+    return float4{(float)a.x * s, (float)a.y * s, (float)a.z * s, (float)a.w * s};
+  };
+  for (; i + (QV_UNROLL - 1) * stride < n4; i += QV_UNROLL * stride) {
+    int4 a[QV_UNROLL];
+#pragma unroll
+    for (int u = 0; u < QV_UNROLL; ++u) a[u] = acc[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < QV_UNROLL; ++u) y[i + u * stride] = dq(a[u], i + u * stride);
+  }
+  for (; i < n4; i += stride) y[i] = dq(acc[i], i);
+}
+
+inline unsigned grid_stream() { return 8u * (unsigned)num_cus_layerops(); }
 
 template <typename T>
 __global__ void nchw_to_nhwc_kernel(const T* __restrict__ x, int N, int C, int HW, int Cs, T* __restrict__ y) {
@@ -152,7 +212,15 @@ int dlq_finalize(void) {
 int dlq_quantize_f32_s8(const float* x, size_t n, float inv_s, int8_t* q, void* stream) {
   if (n == 0) return DLQ_OK;
   if (!x || !q) return fail(DLQ_ERR_ARG, "quantize_f32_s8: null pointer");
-  hipLaunchKernelGGL(quantize_f32_s8_kernel, dim3(grid1(n)), dim3(256), 0, (hipStream_t)stream, x, n, inv_s, q);
+  size_t n4 = 0;
+  if (((uintptr_t)x & 15) == 0 && ((uintptr_t)q & 3) == 0 && n >= 1024) {
+    n4 = n / 4;
+    hipLaunchKernelGGL(quantize_f32_s8_v4_kernel, dim3(grid_stream()), dim3(256), 0, (hipStream_t)stream,
+                       (const float4*)x, n4, inv_s, (unsigned*)q);
+  }
+  if (4 * n4 < n)
+    hipLaunchKernelGGL(quantize_f32_s8_kernel, dim3(grid1(n - 4 * n4)), dim3(256), 0, (hipStream_t)stream, x + 4 * n4,
+                       n - 4 * n4, inv_s, q + 4 * n4);
   return status(launched(), "quantize_f32_s8");
 }
 
@@ -274,8 +342,19 @@ int dlq_dequant_s32_f32(const int32_t* acc, int N, int C, int HW, const float* s
   if (N < 0 || C <= 0 || HW <= 0) return fail(DLQ_ERR_ARG, "dequant: bad shape");
   if (N == 0) return DLQ_OK;
   if (!acc || !scale || !y) return fail(DLQ_ERR_ARG, "dequant: null pointer");
-  hipLaunchKernelGGL(dequant_s32_f32_kernel, dim3(grid1((size_t)N * C * HW)), dim3(256), 0, (hipStream_t)stream,
-                     acc, N, C, HW, scale, y);
+  const size_t total = (size_t)N * C * HW;
+  if (HW % 4 == 0 && ((uintptr_t)acc & 15) == 0 && ((uintptr_t)y & 15) == 0 && total >= 1024) {
+    const size_t n4 = total / 4;
+    if (n4 < 0x7fffffffu)
+      hipLaunchKernelGGL(dequant_s32_f32_v4_kernel<unsigned>, dim3(grid_stream()), dim3(256), 0, (hipStream_t)stream,
+                         (const int4*)acc, (unsigned)n4, (unsigned)(HW / 4), C, scale, (float4*)y);
+    else
+      hipLaunchKernelGGL(dequant_s32_f32_v4_kernel<size_t>, dim3(grid_stream()), dim3(256), 0, (hipStream_t)stream,
+                         (const int4*)acc, n4, (size_t)(HW / 4), C, scale, (float4*)y);
+  } else {
+    hipLaunchKernelGGL(dequant_s32_f32_kernel, dim3(grid1(total)), dim3(256), 0, (hipStream_t)stream, acc, N, C, HW,
+                       scale, y);
+  }
   return status(launched(), "dequant");
 }
 

@@ -216,6 +216,42 @@ def test_bn_relu_add_requant_dequant(gpu):
     assert np.array_equal(yf.cpu().numpy().view(np.int32), ref.view(np.int32))
 
 
+@pytest.mark.parametrize("n,off", [(1023, 0), (1024, 0), (100003, 0), (100003, 4), (100003, 1), (3 * 224 * 224 * 9, 0)])
+def test_quantize_f32_s8_streaming(gpu, n, off):
+    """The 16-byte streaming form of dlq_quantize_f32_s8 (16-byte aligned x,
+    n >= 1024: the vector body + a scalar tail) and the scalar kernel
+    (misaligned x: off floats into the buffer), bit-exact with the oracle
+    (ties, saturation, signed zero)."""
+    from dlq_amd.lib import lib
+    rng = np.random.default_rng(n + off)
+    x = (rng.standard_normal(n, dtype=np.float32) * 3).astype(np.float32)
+    x[:8] = [0.5, 1.5, -2.5, 1e9, -1e9, 0.0, -0.0, 126.5 * 0.021]
+    s = np.float32(0.021)
+    xb = torch.zeros(n + 8, dtype=torch.float32, device="cuda")
+    xb[off:off + n] = torch.from_numpy(x).cuda()
+    q = torch.empty(n, dtype=torch.int8, device="cuda")
+    _ok(lib.dlq_quantize_f32_s8(xb.data_ptr() + 4 * off, n, float(O.inv_scale(s)), _p(q), None))
+    torch.cuda.synchronize()
+    assert np.array_equal(q.cpu().numpy(), O.quantize_f32_s8(x, s))
+
+
+@pytest.mark.parametrize("N,Cc,HW", [(3, 5, 12), (2, 64, 3136), (4, 512, 49), (256, 1000, 1), (1, 7, 4)])
+def test_dequant_s32_f32_streaming(gpu, N, Cc, HW):
+    """dlq_dequant_s32_f32: the 16-byte streaming kernel (HW % 4 == 0, >= 1024
+    elements, 32-bit index math) and the scalar kernel otherwise; y =
+    float(acc) * scale[c] bit for bit."""
+    from dlq_amd.lib import lib
+    rng = np.random.default_rng(N * Cc + HW)
+    acc = rng.integers(-(1 << 24), 1 << 24, size=(N, Cc, HW), dtype=np.int32)
+    acc.flat[:2] = [2**31 - 1, -2**31]
+    scale = (rng.random(Cc, dtype=np.float32) * 1e-2).astype(np.float32)
+    yf = torch.empty(acc.shape, dtype=torch.float32, device="cuda")
+    _ok(lib.dlq_dequant_s32_f32(_p(_cuda(acc)), N, Cc, HW, _p(_cuda(scale)), _p(yf), None))
+    torch.cuda.synchronize()
+    ref = acc.astype(np.float32) * scale[None, :, None]
+    assert np.array_equal(yf.cpu().numpy().view(np.int32), ref.view(np.int32))
+
+
 def test_maxpool_gap_fc_nchw(gpu):
     from dlq_amd import ops
     from dlq_amd.lib import lib

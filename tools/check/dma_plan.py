@@ -25,6 +25,13 @@ for every shape and batch size asked for it proves:
     pointer arithmetic on the kernel's own pointers, so no base is assembled
     from 32-bit halves (the round-2 sign-extension fault).
 
+With emit= a dict, the two checks also return each wave's LDS-DMA pieces in
+issue order -- (LDS address, 64 source codes: kind << 48 | byte offset, kinds
+X input, Z zero block, W conv weights, D downsample weights) per (workgroup,
+wave) -- which tests/test_gpu_dma_plan.py compares with the pieces the
+compiled kernels record in a plan-capture build (tools/check/plan_capture.hip):
+the restatement is pinned to the kernels, not only to itself.
+
 Run: python tools/check/dma_plan.py [N ...]   (tests/test_dma_plan.py runs it)
 """
 from __future__ import annotations
@@ -45,6 +52,13 @@ def xcd_remap(bid, nblk):
 
 class Fail(AssertionError):
     pass
+
+
+KX, KZ, KW, KD = 1, 2, 3, 4  # source kinds of emitted pieces
+
+
+def code(kind, off):
+    return (np.int64(kind) << np.int64(48)) | np.asarray(off, dtype=np.int64)
 
 
 def need(cond, msg):
@@ -77,7 +91,7 @@ def igeo(W, SPS=1):
                 NPIECE=SPS * (WP + PP), OFF_Z=OFF_Z, SLOT=SLOT, OFF_AB=2 * SLOT)
 
 
-def check_conv3x3i(W, N):
+def check_conv3x3i(W, N, emit=None):
     C = {28: 128, 14: 256, 7: 512}[W]
     SPS = 2 if W == 7 else 1  # int8: the 7x7 launches take two 32-channel slices per stage (sps_of)
     g = igeo(W, SPS)
@@ -126,6 +140,7 @@ def check_conv3x3i(W, N):
             o128, ohalf = (ot * OT) >> 7, (ot * OT) & 127
             wbase = (o128 * NSL * 128 + ohalf) * g["IPITCH"]
             for st in range(NS):
+                s_idx = li * NS + st  # the workgroup's stage index (slot s_idx % 2)
                 j0 = st * SPS  # the stage's first slice
                 issued = np.zeros(g["NPIECE"], int)
                 for wv in range(NLD):
@@ -143,6 +158,10 @@ def check_conv3x3i(W, N):
                             dst = g["OFF_P"] + sub * g["PB"] + p * 1024
                             need(dst + 1024 <= g["OFF_Z"] + sub * g["PB"], "patch piece into the zero region")
                             issued[pc] += 1
+                            if emit is not None:
+                                emit.setdefault((b, wv), []).append(
+                                    (s_idx % 2 * g["SLOT"] + dst,
+                                     np.where(s_ok, code(KX, src[us] + j * 32), code(KZ, (lane & 3) * 16 + j * 32))))
                         elif pc < g["PPS"] + g["WPS"]:
                             wp = pc - g["PPS"]
                             sub = 1 if (SPS > 1 and wp >= g["WP"]) else 0
@@ -151,6 +170,9 @@ def check_conv3x3i(W, N):
                             need(s0 >= 0 and s0 + 1024 <= wbytes, "weight piece past the packed image")
                             need(sub * g["WB"] + q * 1024 + 1024 <= g["WBS"], "weight piece past the weight region")
                             issued[pc] += 1
+                            if emit is not None:
+                                emit.setdefault((b, wv), []).append(
+                                    (s_idx % 2 * g["SLOT"] + wp * 1024, code(KW, s0 + 16 * lane)))
                 need(issued == 1, f"conv3x3i W={W}: a piece issued {issued.min()}..{issued.max()} times")
             # tap reads of the item: every output pixel, every tap, both planes
             p = p0 + lp_all
@@ -229,7 +251,7 @@ def make_perm(OW):
     return np.array(px)
 
 
-def check_s2i(OW, N):
+def check_s2i(OW, N, emit=None):
     C = {28: 64, 14: 128, 7: 256}[OW]
     OC, NS, JNW = 2 * C, C // 32, 8
     RW = OW == 28  # layer2.0: resident weights (OCp == JOT)
@@ -248,15 +270,19 @@ def check_s2i(OW, N):
     wbytes_c, wbytes_d = n_ot * NS * g["WB"], n_ot * NS * g["DB"]
     need(xbytes < INT_MAX, f"conv3x3s2i OW={OW}: N={N} overflows the int pixel offset")
     lane = np.arange(64)
+    rw_pieces = []  # (wave, LDS address, codes) of the resident-weight prologue
     if RW:  # resident weights: every stage's block once, pc = wave + 8 i
         NW = NS * g["WP"]
         for pc in range(NW):
             j, qq = pc // g["WP"], pc % g["WP"]
             if qq < WCP:
                 need(j * g["WB"] + qq * 1024 + 1024 <= wbytes_c, "resident conv weight piece past the image")
+                cd = code(KW, j * g["WB"] + qq * 1024 + 16 * lane)
             else:
                 need(j * g["DB"] + (qq - WCP) * 1024 + 1024 <= wbytes_d, "resident ds weight piece past the image")
+                cd = code(KD, j * g["DB"] + (qq - WCP) * 1024 + 16 * lane)
             need(pc * 1024 + 1024 <= g["W_ALL"], "resident weights past their region")
+            rw_pieces.append((pc % JNW, pc * 1024, cd))
     u = np.arange(g["PP"] * 64)
     plane = (u >= g["UP"]).astype(int)
     q = u - plane * g["UP"]
@@ -274,6 +300,9 @@ def check_s2i(OW, N):
     for b in range(Gd):
         bb = xcd_remap(b, Gd)
         nst = ((NI - bb + Gd - 1) // Gd) * NS
+        if emit is not None:
+            for wv, dst, cd in rw_pieces:
+                emit.setdefault((b, wv), []).append((dst, cd))
         for li in range(nst // NS):
             it = bb + li * Gd
             ot, p0 = it % n_ot, (it // n_ot) * g["JL"]
@@ -284,6 +313,7 @@ def check_s2i(OW, N):
             ok = (u < 2 * g["UP"]) & (c < g["IPI"]) & (r < g["IRC"]) & (n < N) & (ih >= 0) & (ih < HI)
             src = np.where(ok, ((n * HI + ih) * WI + iw) * C + plane * 16, -1)
             for j in range(NS):
+                s_idx = li * NS + j  # the workgroup's stage index (slot s_idx % 2)
                 issued = np.zeros(g["NPIECE"], int)
                 for wv in range(JNW):
                     for k in range(DPW):
@@ -295,6 +325,10 @@ def check_s2i(OW, N):
                             need((lane[~s_ok] & 3) * 16 + j * 32 + 16 <= 1024, "zero source past the zero block")
                             need(g["OFF_P"] + pc * 1024 + 1024 <= g["OFF_Z"], "patch piece into the zero region")
                             issued[pc] += 1
+                            if emit is not None:
+                                emit.setdefault((b, wv), []).append(
+                                    (s_idx % 2 * g["SLOT"] + g["OFF_P"] + pc * 1024,
+                                     np.where(s_ok, code(KX, src[us] + j * 32), code(KZ, (lane & 3) * 16 + j * 32))))
                         elif pc < g["PP"] + g["WPC"]:
                             wp = pc - g["PP"]
                             if wp < WCP:
@@ -305,6 +339,9 @@ def check_s2i(OW, N):
                                 need(s0 + 1024 <= wbytes_d, "ds weight piece past the image")
                             need(wp * 1024 + 1024 <= g["OFF_P"], "weight piece into the patch region")
                             issued[pc] += 1
+                            if emit is not None:
+                                emit.setdefault((b, wv), []).append(
+                                    (s_idx % 2 * g["SLOT"] + wp * 1024, code(KW if wp < WCP else KD, s0 + 16 * lane)))
                 need(issued == 1, f"s2i OW={OW}: a piece issued {issued.min()}..{issued.max()} times")
             p = p0 + lp
             valid = real & (p < P)
