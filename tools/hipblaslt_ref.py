@@ -1,7 +1,8 @@
 """Calibration (not product code): the vendor int8 GEMM (torch._int_mm ->
 hipBLASLt on ROCm) at the shapes the round's GEMM numbers are quoted on, next
-to dlq_gemm_s8s8s32, so the kernels' MFMA fraction can be read against what
-the library reaches on the same box at the same loaded clock."""
+to dlq_gemm_s8s8s32 (NN) and dlq_gemm_s8s8s32_nt (NT), so the kernels' MFMA
+fraction can be read against what the library reaches on the same box at the
+same loaded clock."""
 import json
 import os
 import sys
@@ -48,6 +49,13 @@ def main():
             ms = timed(lambda: check(lib.dlq_gemm_s8s8s32(A.data_ptr(), Bn.data_ptr(), C.data_ptr(), M, N, K, st),
                                      "gemm"))
             ent["dlq_gemm_tops"] = round(2.0 * M * N * K / (ms * 1e-3) / 1e12, 1)
+            ms = timed(lambda: check(lib.dlq_gemm_s8s8s32_nt(A.data_ptr(), Bt.data_ptr(), C.data_ptr(), M, N, K, st),
+                                     "gemm_nt"))
+            ent["dlq_gemm_nt_tops"] = round(2.0 * M * N * K / (ms * 1e-3) / 1e12, 1)
+            ref = torch._int_mm(A[:256], Bt.t())
+            check(lib.dlq_gemm_s8s8s32_nt(A.data_ptr(), Bt.data_ptr(), C.data_ptr(), M, N, K, st), "gemm_nt")
+            torch.cuda.synchronize()
+            ent["dlq_nt_equals_int_mm_rows0_255"] = bool(torch.equal(C[:256], ref))
         except Exception as e:
             ent["nn_error"] = repr(e)[:200]
         out[f"{M}x{N}x{K}"] = ent
