@@ -37,8 +37,12 @@ bin/dlq_step: dlq_amd/csrc/main_step.cpp dlq_amd/libdlq.so include/dlq.h
 
 # test infrastructure: the convs' LDS-DMA plans recorded by the kernels
 # themselves (tests/test_gpu_dma_plan.py)
-tools/check/libplancap.so: tools/check/plan_capture.hip dlq_amd/csrc/conv3x3i.hip dlq_amd/csrc/conv3x3s2i.hip $(HDR)
-	$(HIPCC) $(HIPFLAGS) -shared -I dlq_amd/csrc -o $@ $<
+build/plancap%.o: tools/check/plan_capture.hip dlq_amd/csrc/conv3x3i.hip dlq_amd/csrc/conv3x3s2i.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -DPLANCAP_KIND=$* -I dlq_amd/csrc -c -o $@ $<
+
+tools/check/libplancap.so: build/plancap0.o build/plancap1.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle:
 	$(MAKE) -C oracle

@@ -33,7 +33,7 @@ def _capture(kind, W, N):
     lds = np.zeros(nw * MAXREC, np.uint32)
     src = np.zeros(nw * MAXREC * 64, np.uint64)
     bases = np.zeros(4, np.uint64)
-    f = lib.plancap_run
+    f = lib.plancap_run_wide if kind == 0 else lib.plancap_run_s2i
     f.restype = C.c_int
     n = f(C.c_int(kind), C.c_int(W), C.c_int(N), C.c_uint(MAXREC), cnt.ctypes.data_as(C.c_void_p),
           lds.ctypes.data_as(C.c_void_p), src.ctypes.data_as(C.c_void_p), bases.ctypes.data_as(C.c_void_p))

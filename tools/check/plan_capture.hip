@@ -7,8 +7,8 @@
 // wave, in issue order: LDS address + 64 lane sources) with the plans
 // tools/check/dma_plan.py derives, so the host checker cannot drift from the
 // compiled kernels.
-// Build (Makefile): hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared
-//   -I dlq_amd/csrc tools/check/plan_capture.hip -o tools/check/libplancap.so
+// Build (Makefile): compiled twice, -DPLANCAP_KIND=0 (wide) and 1 (stride-2),
+// in parallel, and linked into tools/check/libplancap.so.
 #define DLQ_PLAN_CAPTURE 1
 #include <hip/hip_runtime.h>
 
@@ -16,10 +16,15 @@
 #include <vector>
 
 namespace dlq {
+#if PLANCAP_KIND == 0  // (one definition across the two objects)
 int packed_oc(int OC) { return OC <= 64 ? 64 : (OC + 127) / 128 * 128; }
+#endif
 }  // namespace dlq
+#if PLANCAP_KIND == 0
 #include "../../dlq_amd/csrc/conv3x3i.hip"
+#else
 #include "../../dlq_amd/csrc/conv3x3s2i.hip"
+#endif
 
 using namespace dlq;
 
@@ -36,8 +41,14 @@ hipError_t dmalloc(T** p, size_t bytes) {
 // lds[w * max_rec + i], src[(w * max_rec + i) * 64 + lane]; bases = the
 // device addresses of x, the conv weights, the downsample weights and the
 // kernel's zero block.  Returns the number of waves, or -1 on a HIP error.
-extern "C" int plancap_run(int kind, int W, int N, unsigned max_rec, unsigned* cnt, unsigned* lds,
+#if PLANCAP_KIND == 0
+#define PLANCAP_RUN plancap_run_wide
+#else
+#define PLANCAP_RUN plancap_run_s2i
+#endif
+extern "C" int PLANCAP_RUN(int kind, int W, int N, unsigned max_rec, unsigned* cnt, unsigned* lds,
                            unsigned long long* src, unsigned long long* bases) {
+  if (kind != PLANCAP_KIND) return -1;
   const int C = kind == 0 ? (W == 28 ? 128 : W == 14 ? 256 : 512) : (W == 56 ? 64 : W == 28 ? 128 : 256);
   const int OW = kind == 0 ? W : W / 2, OC = kind == 0 ? C : 2 * C, P = N * OW * OW;
   const size_t xb = (size_t)N * W * W * C, yb = (size_t)P * OC;
@@ -78,13 +89,13 @@ extern "C" int plancap_run(int kind, int W, int N, unsigned max_rec, unsigned* c
   a.out_kind = 0;
   void* zero = nullptr;
   hipError_t e;
-  if (kind == 0) {
-    e = launch_conv3x3i(a, 0);
-    if (e == hipSuccess) e = hipGetSymbolAddress(&zero, HIP_SYMBOL(g_zero_i));
-  } else {
-    e = launch_conv3x3s2i(a, wd, ab + 2 * OC, ab + 3 * OC, yd, 0);
-    if (e == hipSuccess) e = hipGetSymbolAddress(&zero, HIP_SYMBOL(g_zero_s2i));
-  }
+#if PLANCAP_KIND == 0
+  e = launch_conv3x3i(a, 0);
+  if (e == hipSuccess) e = hipGetSymbolAddress(&zero, HIP_SYMBOL(g_zero_i));
+#else
+  e = launch_conv3x3s2i(a, wd, ab + 2 * OC, ab + 3 * OC, yd, 0);
+  if (e == hipSuccess) e = hipGetSymbolAddress(&zero, HIP_SYMBOL(g_zero_s2i));
+#endif
   if (e != hipSuccess || hipDeviceSynchronize() != hipSuccess) return -1;
   std::vector<PlanPiece> h((size_t)nw * max_rec);
   if (hipMemcpy(h.data(), buf, h.size() * sizeof(PlanPiece), hipMemcpyDeviceToHost) ||
@@ -98,13 +109,7 @@ extern "C" int plancap_run(int kind, int W, int N, unsigned max_rec, unsigned* c
   bases[1] = (uintptr_t)w;
   bases[2] = (uintptr_t)wd;
   bases[3] = (uintptr_t)zero;
-  hipFree(x);
-  hipFree(w);
-  hipFree(wd);
-  hipFree(y);
-  hipFree(yd);
-  hipFree(ab);
-  hipFree(buf);
-  hipFree(dcnt);
+  for (void* p : {(void*)x, (void*)w, (void*)wd, (void*)y, (void*)yd, (void*)ab, (void*)buf, (void*)dcnt})
+    (void)hipFree(p);
   return nw;
 }
