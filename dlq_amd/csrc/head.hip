@@ -332,24 +332,19 @@ constexpr int MLP_MR_DEFAULT = 4;
 constexpr int MLP_KB = 26;  // fc1 k-steps per register batch (K = 832)
 constexpr int MLP_W2 = 8;   // fc2 k-steps prefetched at kernel start (H <= 256)
 
-__device__ __forceinline__ v4i mlp_wfrag(const int8_t* wp, size_t ws, int k, int lh, int sw) {
-  const int lc = (2 * k + lh) & 3;  // generic packed image: chunk (2k + lh) & 3 of 64-deep block k >> 1
-  return *(const v4i*)(wp + (size_t)(k >> 1) * ws + ((lc ^ sw) << 4));
+// The fused kernel's weight images are fragment-major (mlp.cpp
+// mlp_fragment_image): fragment (k-step k, 32-channel tile t) is 1 KiB at
+// (k * T + t) * 1024, lane l's 16 bytes at l * 16, so every fragment load of
+// a wave reads one contiguous KiB (the generic packed image spread it over
+// 32 rows: 4x the cache lines per load, and loading the weights was the
+// launch's longest phase).
+__device__ __forceinline__ v4i mlp_frag(const int8_t* wf, int T, int k, int t, int lane) {
+  return *(const v4i*)(wf + ((size_t)k * T + t) * 1024 + lane * 16);
 }
-// n k-steps of fragments from k-step kb on: a wave-uniform block pointer
-// bumped once per 64-deep block (never past the last block) + per-lane 32-bit
-// offsets for even / odd k (row + XOR'd chunk), i.e. a scalar add and a
-// global_load in the saddr form per fragment.  kb and nk are even.
 template <int NF>
-__device__ __forceinline__ void mlp_wfrags(const int8_t* w, size_t ws, int kb, int nk, const unsigned (&offs)[2],
-                                           v4i (&f)[NF]) {
-  const int8_t* wk = w + (size_t)(kb >> 1) * ws;
+__device__ __forceinline__ void mlp_frags(const int8_t* wf, int T, int kb, int nk, int t, int lane, v4i (&f)[NF]) {
 #pragma unroll
-  for (int i = 0; i < NF; i += 2) {
-    f[i] = *(const v4i*)(wk + offs[0]);
-    if (i + 1 < NF) f[i + 1] = *(const v4i*)(wk + offs[1]);
-    wk += kb + i + 2 < nk ? ws : 0;
-  }
+  for (int i = 0; i < NF; ++i) f[i] = mlp_frag(wf, T, kb + i < nk ? kb + i : nk - 1, t, lane);  // never past the last
 }
 
 template <int MLP_MR>  // rows per workgroup (= input float4 loads per thread issued up front)
@@ -366,7 +361,7 @@ __global__ __launch_bounds__(MLP_NW * 64) void mlp_fused_kernel(
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 31, lh = lane >> 5;
   const int r0 = blockIdx.x * MLP_MR, br = lr & (MLP_MR - 1), nrow = min(MLP_MR, N - r0);
   const int T = H / 32, T2 = (OC + 31) / 32, nk1 = kp / 32, nk2 = H / 32, u4 = kp >> 2;
-  const size_t ws1 = (size_t)(OCp1 / 64) * 64 * 64, ws2 = (size_t)(OCp2 / 64) * 64 * 64;
+  const int TI1 = OCp1 / 32, TI2 = OCp2 / 32;  // tiles per k-step in the fragment images
   MSTAMP(0);
 
   // 0. loads, in the order of need (vmcnt counts in issue order)
@@ -378,21 +373,14 @@ __global__ __launch_bounds__(MLP_NW * 64) void mlp_fused_kernel(
     for (int r = 0; r < MLP_MR; ++r)
       f[r] = *(const float4*)((const char*)(x + (size_t)(r0 + min(r, nrow - 1)) * in) + xo);
   }
-  const int oc1 = min(wave, T - 1) * 32 + lr, ol1 = oc1 & 63, sw1 = (ol1 >> 2) & 3;
-  const int oc2 = min(wave, T2 - 1) * 32 + lr, ol2 = oc2 & 63, sw2 = (ol2 >> 2) & 3;
-  const int8_t* wp1 = w1 + ((size_t)(oc1 >> 6) * 64 + ol1) * 64;
-  const int8_t* wp2 = w2 + ((size_t)(oc2 >> 6) * 64 + ol2) * 64;
+  const int t1 = min(wave, T - 1), t2 = min(wave, T2 - 1);  // this wave's first fc1 / fc2 tiles
   // epilogue constants, one of each per thread (to LDS after the quantisation)
   const float ca1 = a1[min(tid, H - 1)], cb1 = b1[min(tid, H - 1)];
   const float ca2 = a2[min(tid, OC - 1)], cb2 = b2[min(tid, OC - 1)];
-  const unsigned o1[2] = {(unsigned)(wp1 - w1) + (unsigned)(((0 + lh) ^ sw1) << 4),
-                          (unsigned)(wp1 - w1) + (unsigned)(((2 + lh) ^ sw1) << 4)};
-  const unsigned o2[2] = {(unsigned)(wp2 - w2) + (unsigned)(((0 + lh) ^ sw2) << 4),
-                          (unsigned)(wp2 - w2) + (unsigned)(((2 + lh) ^ sw2) << 4)};
   v4i fa[MLP_KB];
-  mlp_wfrags(w1, ws1, 0, nk1, o1, fa);
+  mlp_frags(w1, TI1, 0, nk1, t1, lane, fa);
   v4i f2[MLP_W2];
-  mlp_wfrags(w2, ws2, 0, nk2, o2, f2);
+  mlp_frags(w2, TI2, 0, nk2, t2, lane, f2);
   MSTAMP(1);
 
   // 1. quantise the rows into LDS
@@ -438,12 +426,9 @@ __global__ __launch_bounds__(MLP_NW * 64) void mlp_fused_kernel(
 
   // 2. fc1 + bias + ReLU + requant: tiles wave, wave + 4, ...
   for (int ot = wave; ot < T; ot += MLP_NW) {
-    const int oc = ot * 32 + lr, ol = oc & 63, sw = (ol >> 2) & 3;
-    const unsigned ro = (unsigned)(((oc >> 6) * 64 + ol) * 64);
-    const unsigned ot_o[2] = {ro + (unsigned)(((0 + lh) ^ sw) << 4), ro + (unsigned)(((2 + lh) ^ sw) << 4)};
     v16i acc = v16i{0}, acc1 = v16i{0};  // even / odd k-steps: two MFMA chains, summed (exact int32)
     for (int kb = 0; kb < nk1; kb += MLP_KB) {
-      if (kb > 0 || ot != wave) mlp_wfrags(w1, ws1, kb, nk1, ot_o, fa);
+      if (kb > 0 || ot != wave) mlp_frags(w1, TI1, kb, nk1, ot, lane, fa);
 #pragma unroll
       for (int i = 0; i < MLP_KB; ++i)
         if (kb + i < nk1) {  // wave-uniform
@@ -474,17 +459,15 @@ __global__ __launch_bounds__(MLP_NW * 64) void mlp_fused_kernel(
 
   // 3. fc2 + bias -> fp32 logits
   for (int ot = wave; ot < T2; ot += MLP_NW) {
-    const int oc = ot * 32 + lr, ol = oc & 63, sw = (ol >> 2) & 3;
-    const int8_t* wp = w2 + ((size_t)(oc >> 6) * 64 + ol) * 64;
     v16i acc = v16i{0};
 #pragma unroll
     for (int k = 0; k < MLP_W2; ++k)
       if (k < nk2) {
-        const v4i a = ot == wave ? f2[k] : mlp_wfrag(wp, ws2, k, lh, sw);
+        const v4i a = ot == wave ? f2[k] : mlp_frag(w2, TI2, k, ot, lane);
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, *(const v4i*)(hq + br * hp + k * 32 + lh * 16), acc, 0, 0, 0);
       }
     for (int k = MLP_W2; k < nk2; ++k)
-      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(mlp_wfrag(wp, ws2, k, lh, sw),
+      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(mlp_frag(w2, TI2, k, ot, lane),
                                                   *(const v4i*)(hq + br * hp + k * 32 + lh * 16), acc, 0, 0, 0);
     if (lr < nrow) {
 #pragma unroll

@@ -23,8 +23,8 @@ using namespace dlq;
 struct dlq_mlp {
   int in = 0, hidden = 0, out = 0, kp = 0, max_batch = 0;
   float s_in = 1.f, s_hidden = 1.f;
-  int8_t* w1 = nullptr;  // packed [OCp(hidden)][kp]
-  int8_t* w2 = nullptr;  // packed [OCp(out)][hidden]
+  int8_t* w1 = nullptr;  // packed [OCp(hidden)][kp] (fused: its fragment-major image)
+  int8_t* w2 = nullptr;  // packed [OCp(out)][hidden] (fused: its fragment-major image)
   float *a1 = nullptr, *b1 = nullptr, *a2 = nullptr, *b2 = nullptr;
   bool fused = true;      // mlp_fused_fits(kp, hidden, out)
   int8_t* xq = nullptr;  // [max_batch][kp], the three-launch path only
@@ -49,8 +49,28 @@ int up(dlq_mlp* m, void** dst, const void* src, size_t bytes) {
 // rows, packed [OCp][kp]; alpha = s_x * s_w[o], beta = bias[o] -- for an int8
 // output (s_y > 0) both in output-grid units: alpha = (s_x*s_w[o])*(1/s_y),
 // beta = bias[o]*(1/s_y) (the convention of dlq_fold_bn).
+// The fused kernel's fragment-major image of a generic packed [OCp][kp]
+// image (head.hip mlp_frag): fragment (k-step k, tile t) at (k * T + t) *
+// 1024, lane l = 32 lh + r its A-fragment bytes -- row t * 32 + r, k-bytes
+// 32 k + 16 lh .. +15, read where the generic image keeps them (the
+// addressing of the kernels that read it, mlp_wfrag's before): one
+// contiguous KiB per wave-wide fragment load.
+std::vector<int8_t> mlp_fragment_image(const std::vector<int8_t>& g, int OCp, int kp) {
+  const int T = OCp / 32, nk = kp / 32;
+  const size_t ws = (size_t)(OCp / 64) * 64 * 64;
+  std::vector<int8_t> f(g.size());
+  for (int k = 0; k < nk; ++k)
+    for (int t = 0; t < T; ++t)
+      for (int l = 0; l < 64; ++l) {
+        const int oc = t * 32 + (l & 31), lh = l >> 5, ol = oc & 63, sw = (ol >> 2) & 3;
+        const size_t src = (size_t)(k >> 1) * ws + ((size_t)(oc >> 6) * 64 + ol) * 64 + ((((2 * k + lh) & 3) ^ sw) << 4);
+        std::memcpy(&f[((size_t)k * T + t) * 1024 + l * 16], &g[src], 16);
+      }
+  return f;
+}
+
 int prep_layer(dlq_mlp* m, const float* Wt, const float* bias, int in, int out, int kp, float s_x,
-               float s_y, int8_t** dw, float** da, float** db) {
+               float s_y, int8_t** dw, float** da, float** db, bool frag) {
   std::vector<float> w((size_t)out * in);
   for (int i = 0; i < in; ++i)
     for (int o = 0; o < out; ++o) w[(size_t)o * in + i] = Wt[(size_t)i * out + o];
@@ -60,6 +80,7 @@ int prep_layer(dlq_mlp* m, const float* Wt, const float* bias, int in, int out, 
   std::vector<int8_t> packed(packed_bytes(out, kp, 1, 1));
   pack_conv_weights(q.data(), out, in, 1, 1, kp, packed.data());
   const int op = packed_oc(out);
+  if (frag) packed = mlp_fragment_image(packed, op, kp);
   std::vector<float> a(op, 0.f), b(op, 0.f);
   const float inv_y = s_y > 0.f ? 1.0f / s_y : 1.0f;
   for (int o = 0; o < out; ++o) {
@@ -91,8 +112,8 @@ int dlq_mlp_create(int in, int hidden, int out, const float* W1, const float* b1
   m->max_batch = max_batch; m->s_in = s_in; m->s_hidden = s_hidden;
   m->fused = mlp_fused_fits(m->kp, hidden, out);
   int rc;
-  if ((rc = prep_layer(m, W1, b1, in, hidden, m->kp, s_in, s_hidden, &m->w1, &m->a1, &m->b1)) ||
-      (rc = prep_layer(m, W2, b2, hidden, out, hidden, s_hidden, 0.f, &m->w2, &m->a2, &m->b2)) ||
+  if ((rc = prep_layer(m, W1, b1, in, hidden, m->kp, s_in, s_hidden, &m->w1, &m->a1, &m->b1, m->fused)) ||
+      (rc = prep_layer(m, W2, b2, hidden, out, hidden, s_hidden, 0.f, &m->w2, &m->a2, &m->b2, m->fused)) ||
       (!m->fused && (rc = up(m, (void**)&m->xq, nullptr, (size_t)max_batch * m->kp))) ||
       (rc = up(m, (void**)&m->hq, nullptr, (size_t)max_batch * hidden))) {
     dlq_mlp_destroy(m);
