@@ -330,7 +330,9 @@ __device__ unsigned long long g_mlp_stamps[1024 * 4 * 8];
 constexpr int MLP_NW = 4;   // waves
 constexpr int MLP_MR_DEFAULT = 4;
 constexpr int MLP_KB = 26;  // fc1 k-steps per register batch (K = 832)
-constexpr int MLP_W2 = 8;   // fc2 k-steps prefetched at kernel start (H <= 256)
+// fc2 k-steps prefetched at kernel start: the kernel's W2 template argument,
+// H / 32 for H <= 128 (MNIST: 4 -- loading 8 re-read the last fragment four
+// times per wave) and 8 above
 
 // The fused kernel's weight images are fragment-major (mlp.cpp
 // mlp_fragment_image): fragment (k-step k, 32-channel tile t) is 1 KiB at
@@ -347,7 +349,7 @@ __device__ __forceinline__ void mlp_frags(const int8_t* wf, int T, int kb, int n
   for (int i = 0; i < NF; ++i) f[i] = mlp_frag(wf, T, kb + i < nk ? kb + i : nk - 1, t, lane);  // never past the last
 }
 
-template <int MLP_MR>  // rows per workgroup (= input float4 loads per thread issued up front)
+template <int MLP_MR, int MLP_W2>  // rows per workgroup (= input float4 loads per thread issued up front)
 __global__ __launch_bounds__(MLP_NW * 64) void mlp_fused_kernel(
     const float* __restrict__ x, int N, int in, int kp, float inv_s, const int8_t* __restrict__ w1, int H,
     int OCp1, const float* __restrict__ a1, const float* __restrict__ b1, const int8_t* __restrict__ w2, int OC,
@@ -426,20 +428,19 @@ __global__ __launch_bounds__(MLP_NW * 64) void mlp_fused_kernel(
 
   // 2. fc1 + bias + ReLU + requant: tiles wave, wave + 4, ...
   for (int ot = wave; ot < T; ot += MLP_NW) {
-    v16i acc = v16i{0}, acc1 = v16i{0};  // even / odd k-steps: two MFMA chains, summed (exact int32)
+    // k-steps mod 4: four independent MFMA chains (a dependent chain pays the
+    // MFMA's latency per step; this launch is latency-bound), summed (exact int32)
+    v16i ac4[4] = {v16i{0}, v16i{0}, v16i{0}, v16i{0}};
     for (int kb = 0; kb < nk1; kb += MLP_KB) {
       if (kb > 0 || ot != wave) mlp_frags(w1, TI1, kb, nk1, ot, lane, fa);
 #pragma unroll
       for (int i = 0; i < MLP_KB; ++i)
         if (kb + i < nk1) {  // wave-uniform
           const v4i bf = *(const v4i*)(xq + br * xp + (kb + i) * 32 + lh * 16);
-          if (i & 1)
-            acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], bf, acc1, 0, 0, 0);
-          else
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], bf, acc, 0, 0, 0);
+          ac4[i & 3] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], bf, ac4[i & 3], 0, 0, 0);
         }
     }
-    acc += acc1;
+    const v16i acc = (ac4[0] + ac4[1]) + (ac4[2] + ac4[3]);
     if (lr < MLP_MR) {  // D column lr = row r0 + lr
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -507,8 +508,15 @@ hipError_t launch_mlp_mr(const float* x, int N, int in, int kp, float inv_s, con
                          const float* b2, int8_t* hq, float* y, hipStream_t s) {
   const size_t lds = mlp_lds_bytes<MR>(kp, H, OC);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(mlp_fused_kernel<MR>, dim3((N + MR - 1) / MR), dim3(MLP_NW * 64), lds, s, x, N, in, kp, inv_s,
-                     w1, H, packed_oc(H), a1, b1, w2, OC, packed_oc(OC), a2, b2, hq, y);
+if (H <= 64)
+    hipLaunchKernelGGL((mlp_fused_kernel<MR, 2>), dim3((N + MR - 1) / MR), dim3(MLP_NW * 64), lds, s, x, N, in, kp,
+                       inv_s, w1, H, packed_oc(H), a1, b1, w2, OC, packed_oc(OC), a2, b2, hq, y);
+  else if (H <= 128)
+    hipLaunchKernelGGL((mlp_fused_kernel<MR, 4>), dim3((N + MR - 1) / MR), dim3(MLP_NW * 64), lds, s, x, N, in, kp,
+                       inv_s, w1, H, packed_oc(H), a1, b1, w2, OC, packed_oc(OC), a2, b2, hq, y);
+  else
+    hipLaunchKernelGGL((mlp_fused_kernel<MR, 8>), dim3((N + MR - 1) / MR), dim3(MLP_NW * 64), lds, s, x, N, in, kp,
+                       inv_s, w1, H, packed_oc(H), a1, b1, w2, OC, packed_oc(OC), a2, b2, hq, y);
   return hipGetLastError();
 }
 
