@@ -13,8 +13,9 @@ HDR = include/dlq.h dlq_amd/csrc/dlq_internal.h dlq_amd/csrc/device_common.h
 
 all: dlq_amd/libdlq.so bin/dlq_e2e bin/dlq_step tools/check/libplancap.so oracle
 
-# the layer1 block interleaves its epilogue FMAs with MFMAs: keep them scalar
-build/block_l1.o: HIPFLAGS += -fno-slp-vectorize
+# the layer1 block interleaves its epilogue FMAs with MFMAs, and the convs'
+# epilogues run beside the partner waves' MFMAs: keep their FMAs scalar
+build/block_l1.o build/conv3x3i.o build/conv3x3s2i.o: HIPFLAGS += -fno-slp-vectorize
 
 build/%.o: dlq_amd/csrc/%.hip $(HDR)
 	@mkdir -p build

@@ -21,6 +21,7 @@ import argparse
 import json
 import os
 import platform
+import signal
 import socket
 import subprocess
 import sys
@@ -56,36 +57,65 @@ def parse():
     return ap.parse_args()
 
 
+def rank_env(base, r, n, port, threads):
+    """Environment of spawned rank r of n: the torch.distributed.run variables
+    plus OMP_NUM_THREADS = this host's threads / n, so the N ranks' CPU work
+    (calibration, the CPU baseline on rank 0) shares the host instead of
+    each rank starting one thread per host core."""
+    return dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                OMP_NUM_THREADS=str(max(1, threads // n)))
+
+
 def spawn_ranks(n):
     """--gpus N > 1 without a launcher: start N copies of this script as ranks
     0..N-1 of one job (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as
     torch.distributed.run sets them) and return the first non-zero exit
     status, or 0.  The caller has not touched the GPU (each rank is a fresh
-    process; nothing is exec'd in place).  If one rank fails, the others are
-    terminated by PID so the job cannot hang on a missing peer."""
+    process; nothing is exec'd in place).  If one rank fails, or this process
+    is interrupted (Ctrl-C, SIGTERM), every live rank is terminated by PID and
+    killed if it does not exit, so no rank is left holding the GPU or the
+    rendezvous port."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    threads = host_threads()
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+
+    def on_term(signum, frame):
+        raise SystemExit(128 + signum)
+
+    old_term = signal.signal(signal.SIGTERM, on_term)
     rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code
-                for q in live:
-                    q.terminate()
-        if live:
-            time.sleep(0.05)
+    try:
+        for r in range(n):
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                          env=rank_env(os.environ, r, n, port, threads)))
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in live:
+                        q.terminate()
+            if live:
+                time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        signal.signal(signal.SIGTERM, old_term)
     return rc
 
 
@@ -521,7 +551,8 @@ def main():
                    "parallelism": f"dp{world}" if world > 1 else "single",
                    "exchange": ("none" if world == 1 else
                                 "RCCL all_gather_into_tensor of fp32 logits (device tensors)" if backend == "nccl" else
-                                "gloo all_gather of fp32 logits through host tensors (ranks share a GPU)")},
+                                "gloo all_gather of fp32 logits through host tensors (ranks share a GPU)"),
+                   "host_threads_rank0": host_threads()},
         "roofline": {"bound": "mfma", "kernel": FAMILIES[dom],
                      "achieved": round(achieved, 1), "peak": round(PEAK_I8_TOPS, 1),
                      "unit": "TFLOP/s", "int8_ops": not fp8,

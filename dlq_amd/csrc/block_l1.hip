@@ -469,14 +469,9 @@ __global__ __launch_bounds__(512, 1) void block_l1_kernel(BlockArgs a) {
 // compiler-tracked load (conv2 waves issue no LDS-DMA, so the compiler's
 // vmcnt arithmetic is exact for them).
 // The requantisation runs between the MFMAs of the next job: scalar FMAs
-// (device_common.h epi4_relu_s); -DDLQ_L1_PACKED keeps the packed forms.
-#ifdef DLQ_L1_PACKED
+// (device_common.h epi4_relu / epi4_res_relu).
 #define DLQ_L1_EPI epi4_relu
 #define DLQ_L1_EPI_RES epi4_res_relu
-#else
-#define DLQ_L1_EPI epi4_relu_s
-#define DLQ_L1_EPI_RES epi4_res_relu_s
-#endif
 template <bool SECOND>
 __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds, unsigned lds32, int wave, int rows,
                                                  int nphase) {
@@ -550,46 +545,9 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
     rg[3] = rr[3];
   };
 
-  // -DDLQ_X_L1RING: conv2 residuals from the input ring.  In phase g the ring holds input rows
-  // [G-1, G+9) untouched (that phase's DMA refills the slots of rows
-  // [G-9, G-1)), which are exactly the residual rows of phase g+1's outputs
-  // [G-1, G+7) (+ G+7 in the last phase).  So at the end of phase g each
-  // conv2 wave reads its next phase's residual fragments (job k: tile par +
-  // 2k) from the ring into registers, rres[k] (static k: the conv2 job loop
-  // is unrolled over its 8 slots): the consumed slots ahead of the phase's
-  // final epilogue (their latency under its VALU), the last one after it;
-  // all are awaited before the phase barrier.  The block input is then read
-  // from HBM once, by the LDS-DMA (was: + one global re-read per output,
-  // which missed L2).
-#ifdef DLQ_X_L1RING  // measured slower than the L2 re-read so far: a variant build
-  constexpr bool RING_RES = true;
-#else
-  constexpr bool RING_RES = false;
-#endif
-#ifdef DLQ_X_L1UGRES  // A/B probe: the unrolled slot loop with the global residual loads
-  constexpr bool UNROLL = true, GRES = true;
-#else
-  constexpr bool UNROLL = RING_RES, GRES = !RING_RES;
-#endif
-  v4i rres[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) rres[k] = v4i{0, 0, 0, 0};
-  // rres[k] <- job k's residual of the phase after the one at row G
-  auto res_next = [&](int G, auto kc) {
-    constexpr int k = decltype(kc)::value;
-    const int px = (par + 2 * k) * 32 + lr;
-    const int ro = (px * 1171) >> 16;  // px / 56 for px < 512
-    const int col = px - ro * LW;
-    const int R = G - 1 + ro;  // output row of the next phase = input row of its residual
-    // untracked (hipcc would otherwise drain every fragment prefetch with
-    // lgkmcnt(0) waits for it), read into the slot's own register ("+v": the
-    // value never moves while in flight), awaited by the tied wait before the
-    // phase barrier
-    const unsigned addr = lds32 + OFF_IN + (2 * h + lh) * PL + pos_mod(R, NR) * PROW + 16 * (col + 1);
-    v4i& slot = rres[k];
-    asm volatile("ds_read_b128 %0, %1" : "+v"(slot) : "v"(addr) : "memory");
-  };
-
+  // (conv2's residual is re-read from global memory, an L2 hit mostly; the
+  // variant that read it from the LDS input ring cut the launch's HBM bytes
+  // 141 -> 102 MB but ran 1.9 us slower: round-4 DESIGN.md §6, commit e071b4a)
   // the conv2 waves are the critical path (residual epilogues): they win
   // the SIMD's issue arbitration against their conv1 partner, which then
   // spends less of the phase waiting at the barrier
@@ -663,7 +621,7 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
         if (s0 >= NR) s0 -= NR;
         row_addrs(OFF_MID, s0, r, col, valid, jb.ra);
         const size_t pix = valid ? ((size_t)xcd_item(i0, jm) * LW + r) * LW + col : 0;
-        if constexpr (GRES) jb.rq = *(const v4i*)(a.x + pix * LC + h * 32 + lh * 16);
+        jb.rq = *(const v4i*)(a.x + pix * LC + h * 32 + lh * 16);
         jb.dst = valid ? a.y + pix * LC + h * 32 + lh * 16 : g_trash_b + lane * 16;
       }
     };
@@ -677,12 +635,9 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
     Job job[2];
     // job k in set A (acc[A], job[A]); with PREV, job k-1 (set 1 - A) is
     // requantised and stored between the chain's MFMAs
-    // kc: the job slot as a compile-time constant on the ring-residual path
-    auto run = [&](auto ac, auto pc, int k, auto kc) {
+    auto run = [&](auto ac, auto pc, int k) {
       constexpr int A = decltype(ac)::value, E = 1 - A;
       constexpr bool PREV = decltype(pc)::value;
-      constexpr bool RR = SECOND && !GRES;
-      constexpr int KK = decltype(kc)::value;
       if constexpr (SECOND) {  // the first DLQ_L1_PRIOJ jobs of a phase at priority 1
         if (k - kb == 0) __builtin_amdgcn_s_setprio(DLQ_L1_PRIOJ > 0 ? 1 : 0);
         if (k - kb == DLQ_L1_PRIOJ) __builtin_amdgcn_s_setprio(0);
@@ -702,12 +657,7 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
         constexpr int s = decltype(sc)::value;
         if constexpr (s + 2 < KS) ld(std::integral_constant<int, s + 2>{}, (s + 2) % 3);
         if constexpr (PREV) {
-          if constexpr (SECOND && s == 1) {
-            if constexpr (RR)
-              res_regs(rres[KK > 0 ? KK - 1 : 0], rg);
-            else
-              res_regs(job[E].rq, rg);
-          }
+          if constexpr (SECOND && s == 1) res_regs(job[E].rq, rg);
           if constexpr (s == 3 || s == 6 || s == 9 || s == 12) qv[(s - 3) / 3] = epi_group(acc[E], (s - 3) / 3, rg);
           if constexpr (s == 14) finish(mfma_to_store16(qv[0], qv[1], qv[2], qv[3]), job[E]);
         }
@@ -739,53 +689,15 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
     const std::integral_constant<bool, false> NOPREV;
     const std::integral_constant<bool, true> WPREV;
     BT(0);
-    const std::integral_constant<int, -1> NOSLOT;
-    if constexpr (SECOND && UNROLL) {
-      // unrolled over the (at most 8) job slots: job k's residual is rres[k]
-      // and its accumulator set k & 1 (consecutive jobs alternate sets)
-      auto slot = [&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        const std::integral_constant<int, k & 1> IA;
-        if (k >= kb && k < ke) {
-          if constexpr (k == 0)  // slot 0 is always a phase's first job
-            run(IA, NOPREV, k, kc);
-          else if (k == kb)
-            run(IA, NOPREV, k, kc);
-          else
-            run(IA, WPREV, k, kc);
-          if (k == ke - 1) {
-            // every other slot is consumed by now: refill them under the
-            // final epilogue's VALU, then this one
-            if constexpr (!GRES) {
-              auto refill = [&](auto qc) {
-                if (decltype(qc)::value != k) res_next(G, qc);
-              };
-              static_for<0, 8>(refill);
-            }
-            final_epi(IA, GRES ? job[k & 1].rq : rres[k]);
-            if constexpr (!GRES) res_next(G, kc);
-          }
-        }
-      };
-      static_for<0, 8>(slot);
-      if constexpr (!GRES) {
-        if (ke <= kb) {  // no job this phase: every slot
-          auto refill = [&](auto qc) { res_next(G, qc); };
-          static_for<0, 8>(refill);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(rres[0]), "+v"(rres[1]), "+v"(rres[2]), "+v"(rres[3]), "+v"(rres[4]), "+v"(rres[5]),
-                     "+v"(rres[6]), "+v"(rres[7])::"memory");
-    } else if (ke > kb) {  // (a plain branch inside the else of an if constexpr)
-      run(I0, NOPREV, kb, NOSLOT);
+    if (ke > kb) {
+      run(I0, NOPREV, kb);
       int k = kb + 1;
       for (; k + 1 < ke; k += 2) {
-        run(I1, WPREV, k, NOSLOT);
-        run(I0, WPREV, k + 1, NOSLOT);
+        run(I1, WPREV, k);
+        run(I0, WPREV, k + 1);
       }
       if (k < ke) {  // an odd job left: it runs in set 1, the last epilogue is set 1's
-        run(I1, WPREV, k, NOSLOT);
+        run(I1, WPREV, k);
         final_epi(I1, job[1].rq);
       } else {
         final_epi(I0, job[0].rq);
@@ -853,11 +765,7 @@ hipError_t launch_block_l1(const int8_t* x, int N, const int8_t* w1, const float
   if (f8)
     hipLaunchKernelGGL(block_l1_kernel<true>, dim3(N < grid ? N : grid), dim3(512), 0, s, a);
   else
-#ifdef DLQ_X_L1OLD
-    hipLaunchKernelGGL(block_l1_kernel<false>, dim3(N < grid ? N : grid), dim3(512), 0, s, a);
-#else
     hipLaunchKernelGGL(block_l1_sp_kernel, dim3(N < grid ? N : grid), dim3(512), 0, s, a);
-#endif
   return hipGetLastError();
 }
 

@@ -149,44 +149,50 @@ __device__ __forceinline__ void conv3x3i_init(const ConvArgs& a, int8_t* lds) {
       ((int*)(lds + G::SLOT + G::OFF_Z + sub * G::PB))[i] = 0;
     }
   }
-#ifndef DLQ_X_LATEAB
   if constexpr (OUT == 0) {
     for (int i = tid; i < a.OCp; i += INW * 64) {
       ((float*)(lds + G::OFF_AB))[i] = a.alpha[i];
       ((float*)(lds + G::OFF_AB))[C + i] = a.beta[i];
     }
   }
-#endif
 }
 
-// The item stream of one workgroup and its LDS-DMA plan (both bodies below).
-// Items: xcd_chunk over (oc tile, 392-px range), pixel-range major so an
-// XCD's items share input rows.  A stage's pieces are PP patch pieces
-// (per-lane sources: the item's rows; halo units read a zero block) and WP
-// weight pieces (1 KiB blocks of the packed image: a wave-uniform base + 16 *
-// lane, the saddr form).  Loader wave lrank issues pieces lrank + NLD k, patch
-// pieces first; every piece's kind is wave-uniform (a scalar branch, no exec
-// masking) and its LDS destination a constant offset in the slot (weights,
-// then patch).  With SPS slices per stage, patch piece pc is piece pc % PP of
-// the stage's slice pc / PP, weight piece wp piece wp % WP of slice wp / WP.
-template <int W, int C, int SPS, int NLD, int WV>
+// The item stream of one workgroup and its LDS-DMA plan.  A stage's pieces
+// are PPS patch pieces (per-lane sources: the item's rows; halo units read a
+// zero block) and WPS weight pieces (1 KiB blocks of the packed image: a
+// wave-uniform base + 16 * lane, the saddr form).  Wave wv issues patch
+// pieces wv + NLD k at its issue slots k < KPP and weight pieces wv + NLD (k
+// - KPP) at the slots after: the kind of every slot is a compile-time
+// constant shared by all waves, so one code path serves every wave of a pair
+// class (a per-wave instantiation multiplied the code eightfold and thrashed
+// the instruction cache: 20k vs 1.3k SQC_ICACHE_MISSES per launch,
+// profiles/r05_icache2.txt).  A wave with no piece at a slot (index past
+// the stage's count) issues it with EXEC = 0 (glds16_*_m), and with the
+// source and destination of another wave's piece of the same stage (index
+// - count), so even an unmasked issue would only rewrite identical bytes at
+// their own address.  With SPS slices per stage, patch piece pc is piece pc
+// % PP of the stage's slice pc / PP, weight piece wp piece wp % WP of slice
+// wp / WP.
+template <int W, int C, int SPS, int NLD>
 struct WideStream {
   using G = IGeo<W, SPS>;
   static constexpr int H = W, NSL = C / ISC, NS = NSL / SPS;
-  static constexpr int KP = (G::PPS + NLD - 1) / NLD;  // k < KP: possibly a patch piece
-  static constexpr int DPW = (G::NPIECE + NLD - 1) / NLD;  // pieces per loader wave per stage
-  static constexpr int wv = WV;  // this loader wave's rank: every piece's kind is known at compile time
+  static constexpr int KPP = (G::PPS + NLD - 1) / NLD;  // patch slots per wave per stage
+  static constexpr int KPW = (G::WPS + NLD - 1) / NLD;  // weight slots per wave per stage
+  static constexpr int DPW = KPP + KPW;                 // issue slots per wave per stage
+  static_assert(G::PPS >= NLD && G::WPS >= NLD, "an empty slot duplicates piece (index - count)");
   const ConvArgs& a;
-  int n_ot, it0, nit, nst, lane, iss_li = -1;
+  int n_ot, it0, nit, nst, lane, wv, iss_li = -1;
   unsigned lds32;
-  const int8_t* pptr[KP];  // this wave's patch-piece sources for the issuing item's first slice
-  const int8_t* wbase;     // the issuing item's weight blocks (wave-uniform)
+  const int8_t* pptr[KPP];  // this wave's patch-piece sources for the issuing item's first slice
+  const int8_t* wbase;      // the issuing item's weight blocks (wave-uniform)
 
-  __device__ __forceinline__ WideStream(const ConvArgs& a_, int8_t* lds) : a(a_) {
+  __device__ __forceinline__ WideStream(const ConvArgs& a_, int8_t* lds, int wave) : a(a_) {
     n_ot = a.OCp / G::OT;
     xcd_chunk(n_ot * ((a.P + IL - 1) / IL), it0, nit);
     nst = nit * NS;
     lane = threadIdx.x & 63;
+    wv = wave;
     lds32 = lds_addr32(lds);
     wbase = a.w;
   }
@@ -204,8 +210,10 @@ struct WideStream {
     wbase = a.w + (size_t)(o128 * NSL * 128 + ohalf) * IPITCH;
     const int R0 = p0 / W;  // first global output row of the item
 #pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      const int pc = wv + k * NLD, sub = SPS > 1 && pc >= G::PP ? 1 : 0;
+    for (int k = 0; k < KPP; ++k) {
+      int pc = wv + k * NLD;
+      if (pc >= G::PPS) pc -= G::PPS;  // an empty slot: another wave's piece (issued masked)
+      const int sub = SPS > 1 && pc >= G::PP ? 1 : 0;
       const int u = (pc - sub * G::PP) * 64 + lane;
       const int plane = u >= G::UP ? 1 : 0, q = u - plane * G::UP;
       const int c = q / G::CS, rem = q - c * G::CS;
@@ -219,20 +227,20 @@ struct WideStream {
                 sub * ISC;
     }
   }
-  __device__ __forceinline__ void issue(int s, int k) {  // s < nst
+  __device__ __forceinline__ void issue(int s, int k) {  // s < nst; k < DPW (compile-time in every caller)
     const int j0 = (s % NS) * SPS;  // the stage's first slice
-    const int pc = wv + k * NLD;
     const unsigned slot = lds32 + (s & 1) * G::SLOT;
-    if (k < KP && pc < G::PPS) {
+    if (k < KPP) {
+      const int pc0 = wv + k * NLD, pc = pc0 < G::PPS ? pc0 : pc0 - G::PPS;
       const int sub = SPS > 1 && pc >= G::PP ? 1 : 0;
-      glds16_asm(pptr[k < KP ? k : 0] + j0 * ISC, slot + G::OFF_P + sub * G::PB + (pc - sub * G::PP) * 1024);
-    } else if (pc < G::PPS + G::WPS) {
-      const int wp = pc - G::PPS;
+      glds16_asm_m(pptr[k < KPP ? k : 0] + j0 * ISC, slot + G::OFF_P + sub * G::PB + (pc - sub * G::PP) * 1024,
+                   pc0 < G::PPS);
+    } else {
+      const int wp0 = wv + (k - KPP) * NLD, wp = wp0 < G::WPS ? wp0 : wp0 - G::WPS;
       const int8_t* wsl = wbase + (size_t)j0 * 128 * IPITCH;  // the stage's first slice
-      if (SPS == 1 || wp < G::WP)  // a wave-uniform branch per slice keeps each saddr base scalar
-        glds16_saddr(wsl + wp * 1024, (unsigned)lane * 16, slot + wp * 1024);
-      else
-        glds16_saddr(wsl + 128 * IPITCH + (wp - G::WP) * 1024, (unsigned)lane * 16, slot + wp * 1024);
+      // slice 1's block (SPS = 2) sits 128 rows further: a wave-uniform select, no branch
+      const int8_t* wb = SPS == 1 || wp < G::WP ? wsl : wsl + 128 * IPITCH - G::WP * 1024;
+      glds16_saddr_m(wb + wp * 1024, (unsigned)lane * 16, slot + wp * 1024, wp0 < G::WPS);
     }
   }
   __device__ __forceinline__ void prep_for(int s) {
@@ -246,32 +254,29 @@ struct WideStream {
 
 // RELU (int8, OUT == 0): the output clamp is [0, 127] and the requantisation
 // takes the v_cvt_pk_u8_f32 form (device_common.h quant4_relu).
-template <int W, int C, int OUT, bool RES, int NF, int NLD, int WV, bool F8 = false, bool RELU = false>
-__device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int mt, int f0) {
+template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false, bool RELU = false>
+__device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int wave, int mt, int f0) {
   constexpr int SPS = sps_of<W, F8>();
   using G = IGeo<W, SPS>;
   constexpr int NS = C / ISC / SPS;  // stages (SPS 32-channel slices each)
   constexpr int KSN = 9 * SPS;                            // k-steps (tap, slice) per stage
   constexpr int OFF_AB = G::OFF_AB;
-  constexpr int DPW = (G::NPIECE + NLD - 1) / NLD;  // pieces per loader wave per stage
+  constexpr int DPW = WideStream<W, C, SPS, NLD>::DPW;  // issue slots per wave per stage
   static_assert(DPW <= 2 * KSN, "at most two DMA pieces per k-step");
   static_assert(!F8 || SPS == 1, "fp8: one slice per stage");
   static_assert(SPS <= 2, "the piece -> slice selects below");
-  constexpr bool loader = WV < NLD;
+  static_assert(NLD == INW, "every wave issues DMA pieces");
+  constexpr bool loader = true;
   constexpr int STORES = OUT == 0 ? NF : 4 * NF;
   // B fragments two taps ahead for the waves with <= 6 tiles: the younger
   // wave of a SIMD pair runs alone at the end of every stage and, with its
   // fragments only one tap (6 MFMAs) ahead, waited on LDS latency there;
   // the 7-tile waves have no registers to spare for a second set
-#ifdef DLQ_X_PF1
-  constexpr bool PF2 = false;
-#else
   constexpr bool PF2 = NF <= 6;
-#endif
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int lr = lane & 31, lh = lane >> 5;
-  WideStream<W, C, SPS, NLD, WV> st(a, lds);
+  WideStream<W, C, SPS, NLD> st(a, lds, wave);
   const int nst = st.nst;
   auto item_of = [&](int li, int& ot, int& p0) { st.item_of(li, ot, p0); };
   auto issue_piece = [&](int s, int k) { st.issue(s, k); };
@@ -309,16 +314,6 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   }
   conv3x3i_init<W, C, OUT, SPS>(a, lds);
 
-#ifdef DLQ_X_LATEAB
-  // alpha/beta (read only by the epilogue): loaded during stage 0 (their
-  // latency no longer holds up the first barrier), written to LDS before
-  // stage 1's barrier, which publishes them
-  static_assert(C <= INW * 64, "one alpha/beta per thread");
-  float ab_al = 0.f, ab_be = 0.f;
-#endif
-#ifdef DLQ_X_PRIO
-  if (threadIdx.x >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
   // one stage (s < nst); MORE: a stage follows (its DMA is issued in this
   // one).  Two instantiations -- every stage but the last, and the last --
   // so no DMA issue sits behind a runtime branch.
@@ -330,23 +325,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       wait_vm_const<STORES>();
     else
       wait_vm_const<0>();
-#ifdef DLQ_X_LATEAB
-    if constexpr (OUT == 0) {
-      if (s == 1 && tid < a.OCp) {
-        ((float*)(lds + G::OFF_AB))[tid] = ab_al;
-        ((float*)(lds + G::OFF_AB))[C + tid] = ab_be;
-      }
-    }
-#endif
     __builtin_amdgcn_s_barrier();
-#ifdef DLQ_X_LATEAB
-    if constexpr (OUT == 0) {
-      if (s == 0 && tid < a.OCp) {
-        ab_al = a.alpha[tid];
-        ab_be = a.beta[tid];
-      }
-    }
-#endif
     ISTAMP(1 + 2 * s);
     // (fp8: one instantiation with the runtime test -- two spill its registers)
     const bool more = decltype(more_c)::value && (!F8 || s + 1 < nst);
@@ -601,7 +580,11 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
         const bool keep = lp < IL && p < a.P;
         v4i* dst = keep ? (v4i*)((int8_t*)a.y + (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16)
                         : (v4i*)(g_trash_i + lane * 16);
-        *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
+        if (DLQ_ABL(a, 128))  // probe builds: one contiguous KiB per wave-store (store-pattern ablation)
+          dst = (v4i*)((int8_t*)a.y + ((((size_t)blockIdx.x * INW + wave) * 64 + (size_t)(cur_p0 / IL) * 8 + f) * 1024) %
+                                          ((size_t)a.P * a.OC) + lane * 16);
+        if (!DLQ_ABL(a, 64))  // probe builds: dbg 64 drops the int8 stores
+          *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
       }
     }
     };
@@ -627,24 +610,18 @@ __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   int mt, f0, nf;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   wave_tiles<G::MT>(wave, mt, f0, nf);
-  // one instantiation per wave: its DMA pieces' kinds and LDS offsets are
-  // compile-time constants (no scalar branches around the issues)
-  auto go = [&](auto wc) {
-    constexpr int w = decltype(wc)::value;
-    if constexpr (G::MT == 4)
-      conv3x3i_body<W, C, OUT, RES, w < 4 ? 7 : 6, INW, w, F8, RELU>(a, lds, mt, f0);
+  // one instantiation per tile count (the DMA plan's slot kinds are the same
+  // for every wave, WideStream): two bodies per kernel
+  if constexpr (G::MT == 4) {
+    if (wave < 4)
+      conv3x3i_body<W, C, OUT, RES, 7, INW, F8, RELU>(a, lds, wave, mt, f0);
     else
-      conv3x3i_body<W, C, OUT, RES, (w >> 1) == 0 ? 4 : 3, INW, w, F8, RELU>(a, lds, mt, f0);
-  };
-  switch (wave) {
-    case 0: go(std::integral_constant<int, 0>{}); break;
-    case 1: go(std::integral_constant<int, 1>{}); break;
-    case 2: go(std::integral_constant<int, 2>{}); break;
-    case 3: go(std::integral_constant<int, 3>{}); break;
-    case 4: go(std::integral_constant<int, 4>{}); break;
-    case 5: go(std::integral_constant<int, 5>{}); break;
-    case 6: go(std::integral_constant<int, 6>{}); break;
-    default: go(std::integral_constant<int, 7>{}); break;
+      conv3x3i_body<W, C, OUT, RES, 6, INW, F8, RELU>(a, lds, wave, mt, f0);
+  } else {
+    if (wave < 2)
+      conv3x3i_body<W, C, OUT, RES, 4, INW, F8, RELU>(a, lds, wave, mt, f0);
+    else
+      conv3x3i_body<W, C, OUT, RES, 3, INW, F8, RELU>(a, lds, wave, mt, f0);
   }
   (void)nf;
 }

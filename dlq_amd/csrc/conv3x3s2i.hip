@@ -151,19 +151,29 @@ __device__ __forceinline__ int perm_at(int slot) {
 // RELU (int8, OUT == 0): conv1's clamp is [0, 127], requantised in the
 // v_cvt_pk_u8_f32 form (device_common.h quant4_relu); the downsample keeps
 // the signed clamp.
-// WV: this wave's index (compile-time, so each DMA piece's kind and LDS
-// offset are constants: no scalar branches around the issues).
-template <int OW, int C, int OUT, bool DS, int NF, int WV, bool F8, bool RW, bool RELU = false>
+// One body per tile count (NF), shared by the four waves of a pair class:
+// the DMA plan's slot kinds are the same for every wave (see below), so no
+// per-wave instantiation is needed (eight of them thrashed the instruction
+// cache, profiles/r05_icache2.txt).
+template <int OW, int C, int OUT, bool DS, int NF, bool F8, bool RW, bool RELU = false>
 __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, const float* be_ds,
-                                         int8_t* y_ds, int8_t* lds, int mt, int f0) {
+                                         int8_t* y_ds, int8_t* lds, int wave, int mt, int f0) {
   using G = JGeo<OW, DS, RW ? C / JSC : 0>;
   constexpr int NS = C / JSC, OC = 2 * C;
-  constexpr int DPW = (G::NPIECE + JNW - 1) / JNW;
+  // issue slots per wave per stage: patch slots k < KPP (piece wv + 8 k),
+  // then weight slots (weight piece wv + 8 (k - KPP): the conv block, then
+  // the downsample block); a wave with no piece at a slot issues it masked
+  constexpr int KPP = (G::PP + JNW - 1) / JNW;
+  constexpr int KPW = (G::WPC + JNW - 1) / JNW;
+  constexpr int DPW = KPP + KPW;
+  // an empty slot (index past the count) is issued masked, with another
+  // wave's piece (index - count): identical bytes to their own LDS address
+  // even if the mask were ignored
+  static_assert(G::PP >= JNW && (G::WPC == 0 || G::WPC >= JNW), "an empty slot duplicates piece (index - count)");
   static_assert(DPW <= 18, "at most two DMA pieces per tap");
   constexpr int STORES = OUT == 0 ? (DS ? 2 * NF : NF) : 4 * NF;
 
   const int tid = threadIdx.x, lane = tid & 63;
-  constexpr int wave = WV;
   const int lr = lane & 31, lh = lane >> 5;
   const int n_ot = a.OCp / JOT;
   const int NI = n_ot * ((a.P + JL - 1) / JL);
@@ -179,14 +189,12 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
   };
 
   // ---- DMA plan (as in conv3x3i.hip): PP patch pieces (per-lane sources,
-  // halo units from a zero block) then WPC weight pieces (conv block, then
-  // downsample block: a wave-uniform base + 16 * lane, the saddr form); wave
-  // w issues pieces w + 8k, each of wave-uniform kind, to a constant offset
-  // in the slot.
-  constexpr int KP = (G::PP + JNW - 1) / JNW;  // k < KP: possibly a patch piece
+  // halo units from a zero block) and WPC weight pieces (conv block, then
+  // downsample block: a wave-uniform base + 16 * lane, the saddr form)
+  constexpr int KP = KPP;
   constexpr int WCP = G::WB / 1024;            // conv weight pieces (then ds pieces)
-  constexpr int wv = WV;
-  const int8_t* pptr[KP];
+  const int wv = wave;
+  const int8_t* pptr[KP > 0 ? KP : 1];
   const int8_t* wb_c = a.w;   // the issuing item's conv / downsample weight blocks (wave-uniform)
   const int8_t* wb_d = w_ds;
   int iss_li = -1;
@@ -198,7 +206,8 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     const int R0 = p0 / OW;  // first global output row
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
-      const int u = (wv + k * JNW) * 64 + lane;
+      const int pc0 = wv + k * JNW, pc = pc0 < G::PP ? pc0 : pc0 - G::PP;  // empty slot: another wave's piece
+      const int u = pc * 64 + lane;
       const int plane = u >= G::UP ? 1 : 0, q = u - plane * G::UP;
       const int c = q / G::CS, rem = q - c * G::CS;
       const int r = rem / G::WI, pos = rem - r * G::WI;
@@ -210,18 +219,17 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
       pptr[k] = ok ? a.x + (size_t)(((n * G::HI + ih) * G::WI + iw) * C + plane * 16) : g_zero_s2i + (lane & 3) * 16;
     }
   };
-  auto issue_piece = [&](int s, int k) {  // s < nst
+  auto issue_piece = [&](int s, int k) {  // s < nst; k < DPW (compile-time in every caller)
     const int j = s % NS;
-    const int pc = wv + k * JNW;
     const unsigned slot = lds32 + (s & 1) * G::SLOT;
-    if (k < KP && pc < G::PP) {
-      glds16_asm(pptr[k < KP ? k : 0] + j * JSC, slot + G::OFF_P + pc * 1024);
-    } else if (pc < G::PP + G::WPC) {
-      const int wp = pc - G::PP;
-      if (wp < WCP)
-        glds16_saddr(wb_c + (size_t)j * G::WB + wp * 1024, (unsigned)lane * 16, slot + wp * 1024);
-      else
-        glds16_saddr(wb_d + (size_t)j * G::DB + (wp - WCP) * 1024, (unsigned)lane * 16, slot + wp * 1024);
+    if (k < KPP) {
+      const int pc0 = wv + k * JNW, pc = pc0 < G::PP ? pc0 : pc0 - G::PP;
+      glds16_asm_m(pptr[k < KP ? k : 0] + j * JSC, slot + G::OFF_P + pc * 1024, pc0 < G::PP);
+    } else {
+      const int wp0 = wv + (k - KPP) * JNW, wp = wp0 < G::WPC ? wp0 : wp0 - G::WPC;
+      // the conv block, or the downsample block (a wave-uniform select, no branch)
+      const int8_t* wb = wp < WCP ? wb_c + (size_t)j * G::WB : wb_d + (size_t)j * G::DB - WCP * 1024;
+      glds16_saddr_m(wb + wp * 1024, (unsigned)lane * 16, slot + wp * 1024, wp0 < G::WPC);
     }
   };
   auto prep_for = [&](int s) {
@@ -253,7 +261,6 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
 
   auto init = [&]() {  // LDS constants after the first DMA issue: their load latency overlaps it
     const int t = threadIdx.x;
-#ifndef DLQ_X_LATEAB
     if constexpr (OUT == 0) {
       float* ab = (float*)(lds + G::OFF_AB);
       for (int i = t; i < a.OCp; i += JNW * 64) {
@@ -265,7 +272,6 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
         }
       }
     }
-#endif
     for (int i = t; i < G::ZU * 4; i += JNW * 64) {
       ((int*)(lds + G::OFF_Z))[i] = 0;
       ((int*)(lds + G::SLOT + G::OFF_Z))[i] = 0;
@@ -289,15 +295,6 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
   init();  // published by stage 0's barrier
   JSTAMP(57);
 
-#ifdef DLQ_X_LATEAB
-  // alpha/beta (read only by the epilogues): loaded during stage 0, written to
-  // LDS before stage 1's barrier (NS >= 2), which publishes them
-  static_assert(OC <= JNW * 64, "one alpha/beta per thread");
-  float ab_v[DS ? 4 : 2] = {};
-#endif
-#ifdef DLQ_X_PRIO
-  if (threadIdx.x >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
   // one stage (s < nst); MORE: a stage follows (its DMA is issued in this
   // one).  int8: every stage but the last, and the last, as two
   // instantiations, so no DMA issue sits behind a runtime branch.
@@ -309,32 +306,7 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     else
       wait_vm_const<0>();
     if (s == 0) JSTAMP(59);
-#ifdef DLQ_X_LATEAB
-    if constexpr (OUT == 0) {
-      if (s == 1 && tid < a.OCp) {
-        float* ab = (float*)(lds + G::OFF_AB);
-        ab[tid] = ab_v[0];
-        ab[OC + tid] = ab_v[1];
-        if constexpr (DS) {
-          ab[2 * OC + tid] = ab_v[2];
-          ab[3 * OC + tid] = ab_v[3];
-        }
-      }
-    }
-#endif
     __builtin_amdgcn_s_barrier();
-#ifdef DLQ_X_LATEAB
-    if constexpr (OUT == 0) {
-      if (s == 0 && tid < a.OCp) {
-        ab_v[0] = a.alpha[tid];
-        ab_v[1] = a.beta[tid];
-        if constexpr (DS) {
-          ab_v[2] = al_ds[tid];
-          ab_v[3] = be_ds[tid];
-        }
-      }
-    }
-#endif
     JSTAMP(1 + 2 * s);
     // (fp8: one instantiation with the runtime test -- two spill its registers)
     const bool more = decltype(more_c)::value && (!F8 || s + 1 < nst);
@@ -515,7 +487,11 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
           const bool keep = !(e & 0x4000) && p < a.P && !no_store;
           v4i* dst = keep ? (v4i*)(out + (size_t)p * a.OC + cur_ot * JOT + mt * 32 + lh * 16)
                           : (v4i*)(g_trash_s2i + lane * 16);
-          *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
+          if (DLQ_ABL(a, 128))  // probe builds: one contiguous KiB per wave-store (store-pattern ablation)
+            dst = (v4i*)(out + ((((size_t)blockIdx.x * JNW + wave) * 64 + (size_t)(cur_p0 / JL) * 8 + f) * 1024) %
+                                   ((size_t)a.P * a.OC) + lane * 16);
+          if (!DLQ_ABL(a, 64))  // probe builds: dbg 64 drops the int8 stores
+            *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
         }
       };
       constexpr float LO = F8 ? -448.f : -127.f;
@@ -546,20 +522,11 @@ __global__ __launch_bounds__(JNW * 64, 1) void conv3x3s2i_kernel(ConvArgs a, con
   static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  auto go = [&](auto wc) {  // one instantiation per wave (see s2i_body)
-    constexpr int w = decltype(wc)::value;
-    s2i_body<OW, C, OUT, DS, w < 4 ? 4 : 3, w, F8, RW, RELU>(a, w_ds, al_ds, be_ds, y_ds, lds, w & 3, w < 4 ? 0 : 4);
-  };
-  switch (wave) {
-    case 0: go(std::integral_constant<int, 0>{}); break;
-    case 1: go(std::integral_constant<int, 1>{}); break;
-    case 2: go(std::integral_constant<int, 2>{}); break;
-    case 3: go(std::integral_constant<int, 3>{}); break;
-    case 4: go(std::integral_constant<int, 4>{}); break;
-    case 5: go(std::integral_constant<int, 5>{}); break;
-    case 6: go(std::integral_constant<int, 6>{}); break;
-    default: go(std::integral_constant<int, 7>{}); break;
-  }
+  // waves 0-3: pixel tiles [0,4) of oc tile w; waves 4-7: tiles [4,7)
+  if (wave < 4)
+    s2i_body<OW, C, OUT, DS, 4, F8, RW, RELU>(a, w_ds, al_ds, be_ds, y_ds, lds, wave, wave & 3, 0);
+  else
+    s2i_body<OW, C, OUT, DS, 3, F8, RW, RELU>(a, w_ds, al_ds, be_ds, y_ds, lds, wave, wave & 3, 4);
 }
 
 int num_cus_s2i() {

@@ -45,34 +45,23 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 
 // Fused epilogue of 4 accumulators (one MFMA-layout register group):
 // y = fma(float(acc), alpha, beta) [+ fma(float(res byte), r_s, y)], then
-// quant4.  The fmas and the rounding add run as packed FP32 pairs
-// (v_pk_fma_f32 / v_pk_add_f32: the same IEEE operations per element, so
-// bit-identical to the scalar sequence and to oracle.c).
+// quant4 -- scalar FMAs, bit-identical to oracle.c.  The kernel files that
+// use them are compiled with -fno-slp-vectorize (Makefile): packed
+// v_pk_fma_f32 forms cost more beside the partner wave's MFMAs
+// (MI355X_MICROARCH.md, 'price of one filler'); measured on the network:
+// stride-2 family 35.1 -> 34.3 us per launch, logits bit-identical
+// (profiles/r05_ab_episc.txt).
 __device__ __forceinline__ unsigned epi4(const int* acc, const float* al, const float* be, float lo) {
-  const v2f y01 = __builtin_elementwise_fma(v2f{(float)acc[0], (float)acc[1]}, v2f{al[0], al[1]}, v2f{be[0], be[1]});
-  const v2f y23 = __builtin_elementwise_fma(v2f{(float)acc[2], (float)acc[3]}, v2f{al[2], al[3]}, v2f{be[2], be[3]});
-  v2f c01 = {__builtin_amdgcn_fmed3f(y01[0], lo, 127.f), __builtin_amdgcn_fmed3f(y01[1], lo, 127.f)};
-  v2f c23 = {__builtin_amdgcn_fmed3f(y23[0], lo, 127.f), __builtin_amdgcn_fmed3f(y23[1], lo, 127.f)};
-  const v2f M = {12582912.0f, 12582912.0f};
-  c01 = c01 + M;
-  c23 = c23 + M;
-  return __builtin_amdgcn_perm(__float_as_uint(c01[1]), __float_as_uint(c01[0]), 0x0c0c0400u) |
-         __builtin_amdgcn_perm(__float_as_uint(c23[1]), __float_as_uint(c23[0]), 0x04000c0cu);
+  return quant4(__builtin_fmaf((float)acc[0], al[0], be[0]), __builtin_fmaf((float)acc[1], al[1], be[1]),
+                __builtin_fmaf((float)acc[2], al[2], be[2]), __builtin_fmaf((float)acc[3], al[3], be[3]), lo);
 }
 __device__ __forceinline__ unsigned epi4_res(const int* acc, const float* al, const float* be, unsigned r4, float r_s,
                                              float lo) {
-  const v2f s = {r_s, r_s};
-  v2f y01 = __builtin_elementwise_fma(v2f{(float)acc[0], (float)acc[1]}, v2f{al[0], al[1]}, v2f{be[0], be[1]});
-  v2f y23 = __builtin_elementwise_fma(v2f{(float)acc[2], (float)acc[3]}, v2f{al[2], al[3]}, v2f{be[2], be[3]});
-  y01 = __builtin_elementwise_fma(v2f{(float)(int)(signed char)r4, (float)(int)(signed char)(r4 >> 8)}, s, y01);
-  y23 = __builtin_elementwise_fma(v2f{(float)(int)(signed char)(r4 >> 16), (float)((int)r4 >> 24)}, s, y23);
-  v2f c01 = {__builtin_amdgcn_fmed3f(y01[0], lo, 127.f), __builtin_amdgcn_fmed3f(y01[1], lo, 127.f)};
-  v2f c23 = {__builtin_amdgcn_fmed3f(y23[0], lo, 127.f), __builtin_amdgcn_fmed3f(y23[1], lo, 127.f)};
-  const v2f M = {12582912.0f, 12582912.0f};
-  c01 = c01 + M;
-  c23 = c23 + M;
-  return __builtin_amdgcn_perm(__float_as_uint(c01[1]), __float_as_uint(c01[0]), 0x0c0c0400u) |
-         __builtin_amdgcn_perm(__float_as_uint(c23[1]), __float_as_uint(c23[0]), 0x04000c0cu);
+  float y[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    y[e] = __builtin_fmaf((float)(int)(signed char)(r4 >> (8 * e)), r_s, __builtin_fmaf((float)acc[e], al[e], be[e]));
+  return quant4(y[0], y[1], y[2], y[3], lo);
 }
 
 // ReLU requantisation without the med3 / magic-number / perm sequence:
@@ -87,32 +76,11 @@ __device__ __forceinline__ unsigned quant4_relu(float y0, float y1, float y2, fl
   return __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(y3, 127.f), 3, r);
 }
 __device__ __forceinline__ unsigned epi4_relu(const int* acc, const float* al, const float* be) {
-  const v2f y01 = __builtin_elementwise_fma(v2f{(float)acc[0], (float)acc[1]}, v2f{al[0], al[1]}, v2f{be[0], be[1]});
-  const v2f y23 = __builtin_elementwise_fma(v2f{(float)acc[2], (float)acc[3]}, v2f{al[2], al[3]}, v2f{be[2], be[3]});
-  return quant4_relu(y01[0], y01[1], y23[0], y23[1]);
-}
-__device__ __forceinline__ unsigned epi4_res_relu(const int* acc, const float* al, const float* be, unsigned r4,
-                                                  float r_s) {
-  const v2f s = {r_s, r_s};
-  v2f y01 = __builtin_elementwise_fma(v2f{(float)acc[0], (float)acc[1]}, v2f{al[0], al[1]}, v2f{be[0], be[1]});
-  v2f y23 = __builtin_elementwise_fma(v2f{(float)acc[2], (float)acc[3]}, v2f{al[2], al[3]}, v2f{be[2], be[3]});
-  y01 = __builtin_elementwise_fma(v2f{(float)(int)(signed char)r4, (float)(int)(signed char)(r4 >> 8)}, s, y01);
-  y23 = __builtin_elementwise_fma(v2f{(float)(int)(signed char)(r4 >> 16), (float)((int)r4 >> 24)}, s, y23);
-  return quant4_relu(y01[0], y01[1], y23[0], y23[1]);
-}
-
-// Scalar-FMA twins of epi4_relu / epi4_res_relu for epilogues interleaved
-// with MFMA chains (block_l1_sp_kernel): beside an MFMA a v_pk_fma_f32 costs
-// ~22 cycles more than the two v_fma_f32 it replaces (MI355X_MICROARCH.md,
-// 'price of one filler'), so there the packed form is an anti-lever.  The
-// same per-element IEEE ops, so bit-identical.  The file that uses them is
-// compiled with -fno-slp-vectorize so the compiler does not re-pack them.
-__device__ __forceinline__ unsigned epi4_relu_s(const int* acc, const float* al, const float* be) {
   return quant4_relu(__builtin_fmaf((float)acc[0], al[0], be[0]), __builtin_fmaf((float)acc[1], al[1], be[1]),
                      __builtin_fmaf((float)acc[2], al[2], be[2]), __builtin_fmaf((float)acc[3], al[3], be[3]));
 }
-__device__ __forceinline__ unsigned epi4_res_relu_s(const int* acc, const float* al, const float* be, unsigned r4,
-                                                    float r_s) {
+__device__ __forceinline__ unsigned epi4_res_relu(const int* acc, const float* al, const float* be, unsigned r4,
+                                                  float r_s) {
   float y[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e)
@@ -175,21 +143,12 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 // slower per launch, tools/ab.py on one box).
 __device__ __forceinline__ void xcd_chunk(int n_items, int& first, int& count) {
   const int Gd = gridDim.x, b = xcd_remap(blockIdx.x, Gd);
-#ifdef DLQ_X_XCDIMG
-  first = (int)((long long)b * n_items / Gd);
-  count = (int)((long long)(b + 1) * n_items / Gd) - first;
-#else
   first = b;
   count = n_items > b ? (n_items - b + Gd - 1) / Gd : 0;
-#endif
 }
 // item index of the block's li-th item under xcd_chunk
 __device__ __forceinline__ int xcd_item(int first, int li) {
-#ifdef DLQ_X_XCDIMG
-  return first + li;
-#else
   return first + li * (int)gridDim.x;
-#endif
 }
 
 // One 16-byte LDS-DMA per lane: global (per-lane address) -> LDS at the
@@ -219,12 +178,19 @@ struct PlanPiece {
 __device__ PlanPiece* g_cap_buf;
 __device__ unsigned* g_cap_cnt;
 __device__ unsigned g_cap_max;
+__device__ unsigned g_cap_nw;    // waves the host sized g_cap_cnt / g_cap_buf for
+__device__ unsigned g_cap_drop;  // pieces not recorded (wave or record index out of range)
 __device__ __forceinline__ void plan_capture(const void* gsrc, unsigned lds_addr) {
   const int lane = threadIdx.x & 63;
   const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (w >= g_cap_nw) {  // a grid larger than the host's buffers: count, never write past them
+    if (lane == 0) atomicAdd(&g_cap_drop, 1u);
+    return;
+  }
   unsigned i = 0;
   if (lane == 0) i = atomicAdd(&g_cap_cnt[w], 1u);
   i = (unsigned)__shfl((int)i, 0);
+  if (i >= g_cap_max && lane == 0) atomicAdd(&g_cap_drop, 1u);
   if (i < g_cap_max) {
     PlanPiece* r = g_cap_buf + (size_t)w * g_cap_max + i;
     r->src[lane] = (unsigned long long)(uintptr_t)gsrc;
@@ -252,6 +218,49 @@ __device__ __forceinline__ void glds16_saddr(const void* base, unsigned voff, un
   return;
 #endif
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(base), "{m0}"(m0) : "memory");
+}
+
+// Predicated twins of glds16_asm / glds16_saddr for piece plans whose kind
+// at each issue slot is the same for every wave (one code path for all waves
+// of a workgroup): a wave with no piece at this slot issues the instruction
+// with EXEC = 0 (no lane reads or writes anything; `gsrc` / `base` must
+// still be an address the wave could read).  No branch is involved, so the
+// surrounding MFMA / LDS schedule (sched_group_barrier) stays one block.  Every
+// counted wait in the kernels covers only VM ops YOUNGER than the awaited one
+// (stores, residual loads), so whether the hardware counts a masked piece in
+// vmcnt cannot change what those waits guarantee.  EXEC is SET to the mask
+// (the ballot of `valid`: all active lanes or none), never AND-ed: an
+// s_and_b64 writes SCC, which the compiler may hold live across the asm (it
+// faulted an s_cselect-chosen address on the GPU); s_mov_b64 leaves SCC.
+__device__ __forceinline__ void glds16_asm_m(const void* gsrc, unsigned lds_addr, bool valid) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
+#ifdef DLQ_PLAN_CAPTURE
+  if (valid) plan_capture(gsrc, m0);
+  return;
+#endif
+  const unsigned long long mask = __builtin_amdgcn_ballot_w64(valid);  // an SGPR pair: all lanes or none
+  unsigned long long saved;
+  asm volatile(
+      "s_mov_b64 %0, exec\n\ts_mov_b64 exec, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(saved)
+      : "v"(gsrc), "{m0}"(m0), "s"(mask)
+      : "memory");
+}
+__device__ __forceinline__ void glds16_saddr_m(const void* base, unsigned voff, unsigned lds_addr, bool valid) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
+#ifdef DLQ_PLAN_CAPTURE
+  if (valid) plan_capture((const char*)base + voff, m0);
+  return;
+#endif
+  const unsigned long long mask = __builtin_amdgcn_ballot_w64(valid);  // an SGPR pair: all lanes or none
+  unsigned long long saved;
+  asm volatile(
+      "s_mov_b64 %0, exec\n\ts_mov_b64 exec, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(saved)
+      : "v"(voff), "s"(base), "{m0}"(m0), "s"(mask)
+      : "memory");
 }
 
 // LDS byte address of a __shared__ pointer (for M0).

@@ -50,7 +50,9 @@ constexpr int kMaxBatch = 8192;
 constexpr int kStemC = 4;
 constexpr int kStemK = 8 * 8 * 4;
 
-int packed_oc(int OC);
+// output channels of a packed weight image (64, or a multiple of 128): the
+// one definition every launcher, packer and test library shares
+inline int packed_oc(int OC) { return OC <= 64 ? 64 : (OC + 127) / 128 * 128; }
 bool is_stem(int C, int kH, int kW);
 
 // Kernel launchers (kernels.hip, conv3x3.hip).  Return hipError_t of the launch.

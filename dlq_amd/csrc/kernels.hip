@@ -465,7 +465,6 @@ inline int grid_for(long total, int per_block = 256) {
 
 }  // namespace
 
-int packed_oc(int OC) { return OC <= 64 ? 64 : (OC + 127) / 128 * 128; }
 bool is_stem(int C, int kH, int kW) { return C == kStemC && kH == 7 && kW == 7; }
 
 hipError_t launch_conv(const ConvArgs& a, hipStream_t s) {

@@ -792,11 +792,7 @@ hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float
   if (f8)
     hipLaunchKernelGGL(stem_fused_kernel<true>, dim3(grid), dim3(SNW * 64), 0, s, a);
   else
-#ifdef DLQ_X_STEM1
-    hipLaunchKernelGGL(stem_fused_kernel<false>, dim3(grid), dim3(SNW * 64), 0, s, a);
-#else
     hipLaunchKernelGGL(stem2_kernel, dim3(grid), dim3(S2W * 64), 0, s, a);
-#endif
   return hipGetLastError();
 }
 

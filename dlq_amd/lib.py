@@ -23,7 +23,10 @@ DLQ_OK = 0
 DLQ_OUT_S8, DLQ_OUT_F32, DLQ_OUT_S32 = 0, 1, 2
 DLQ_PREC_INT8, DLQ_PREC_FP8 = 0, 1
 # kernel families of dlq_resnet18_timing (include/dlq.h DLQ_FAM_*)
-FAMILIES = ["stem_fused_kernel", "block_l1_kernel (layer1 block)", "conv3x3s2i_kernel (+downsample)",
+# (the first word names the int8 forward's kernel; the fp8 forward runs
+# stem_fused_kernel and block_l1_kernel in families 0 and 1)
+FAMILIES = ["stem2_kernel (int8 stem; fp8: stem_fused_kernel)",
+            "block_l1_sp_kernel (int8 layer1 block; fp8: block_l1_kernel)", "conv3x3s2i_kernel (+downsample)",
             "conv3x3i_kernel (layer2-4 s1)", "head: gap_fc_kernel (int8 GAP+FC) / gap16 (fp8, split)", "linear_kernel (fc: fp8 / split head)", "other",
             "conv_s8_kernel fp8 (all convs, fp8 path)"]
 

@@ -72,3 +72,44 @@ def test_bench_gpus2_spawns_two_ranks(gpu):
     dt = out["ms_per_step"] * steps / 1e3
     assert out["value"] == pytest.approx(2 * 256 * steps / dt, rel=2e-3)
     assert "cpu_baseline" not in out  # rank 0 at N = 1 only
+    # each spawned rank gets its share of the host's threads (bench.rank_env)
+    sys.path.insert(0, ROOT)
+    import bench
+    assert out["config"]["host_threads_rank0"] == max(1, bench.host_threads() // 2)
+
+
+def test_rank_env_splits_host_threads():
+    sys.path.insert(0, ROOT)
+    import bench
+    env = bench.rank_env({"PATH": "/bin"}, 3, 8, 29500, 256)
+    assert env["RANK"] == "3" and env["LOCAL_RANK"] == "3" and env["WORLD_SIZE"] == "8"
+    assert env["MASTER_ADDR"] == "127.0.0.1" and env["MASTER_PORT"] == "29500"
+    assert env["OMP_NUM_THREADS"] == "32" and env["PATH"] == "/bin"
+    assert bench.rank_env({}, 0, 8, 1, 4)["OMP_NUM_THREADS"] == "1"
+
+
+def test_spawn_ranks_kills_children_on_interrupt(tmp_path):
+    """An interrupted parent leaves no rank behind (spawn_ranks' finally)."""
+    script = tmp_path / "parent.py"
+    script.write_text(
+        "import sys, os, signal, threading\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import bench, subprocess\n"
+        "bench.__file__ = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'child.py')\n"
+        "threading.Timer(2.0, lambda: os.kill(os.getpid(), signal.SIGTERM)).start()\n"
+        "sys.exit(bench.spawn_ranks(2))\n")
+    (tmp_path / "child.py").write_text(
+        "import os, time\n"
+        "open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'pid%s' % os.environ['RANK']), 'w')"
+        ".write(str(os.getpid()))\n"
+        "time.sleep(120)\n")
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 128 + 15, r.stderr[-2000:]
+    for rank in (0, 1):
+        pid = int((tmp_path / f"pid{rank}").read_text())
+        alive = True
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            alive = False
+        assert not alive, f"rank {rank} (pid {pid}) outlived the parent"

@@ -36,7 +36,10 @@ def _capture(kind, W, N):
     f = lib.plancap_run_wide if kind == 0 else lib.plancap_run_s2i
     f.restype = C.c_int
     n = f(C.c_int(kind), C.c_int(W), C.c_int(N), C.c_uint(MAXREC), cnt.ctypes.data_as(C.c_void_p),
-          lds.ctypes.data_as(C.c_void_p), src.ctypes.data_as(C.c_void_p), bases.ctypes.data_as(C.c_void_p))
+          lds.ctypes.data_as(C.c_void_p), src.ctypes.data_as(C.c_void_p), bases.ctypes.data_as(C.c_void_p),
+          C.c_int(nw))
+    assert n != -2, "plan capture dropped pieces (a wave past the capture buffers, or more than MAXREC pieces)"
+    assert n != -3, "the launch has more waves than the capture arrays hold"
     assert n > 0, "plan capture launch failed"
     return n, cnt[:n], lds[:n * MAXREC].reshape(n, MAXREC), src[:n * MAXREC * 64].reshape(n, MAXREC, 64), bases
 

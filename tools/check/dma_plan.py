@@ -102,8 +102,12 @@ def check_conv3x3i(W, N, emit=None):
     n_ot, n_pi = OCp // OT, (P + IL - 1) // IL
     NI = n_ot * n_pi
     Gd = min(NI, NCU)
-    DPW = (g["NPIECE"] + NLD - 1) // NLD
-    KP = (g["PPS"] + NLD - 1) // NLD
+    # WideStream: patch slots k < KPP (piece wv + NLD k), weight slots after
+    # (piece wv + NLD (k - KPP)); a wave with no piece at a slot issues it
+    # masked (EXEC = 0: nothing is read or written, nothing is recorded)
+    KPP = (g["PPS"] + NLD - 1) // NLD
+    KPW = (g["WPS"] + NLD - 1) // NLD
+    DPW = KPP + KPW
     lds_total = g["OFF_AB"] + 2 * C * 4
     need(lds_total <= 160 * 1024, "LDS budget")
     xbytes = P * C
@@ -145,8 +149,9 @@ def check_conv3x3i(W, N, emit=None):
                 issued = np.zeros(g["NPIECE"], int)
                 for wv in range(NLD):
                     for k in range(DPW):
-                        pc = wv + k * NLD
-                        if k < KP and pc < g["PPS"]:
+                        pc = wv + k * NLD if k < KPP else None
+                        wp = wv + (k - KPP) * NLD if k >= KPP else None
+                        if pc is not None and pc < g["PPS"]:
                             sub = 1 if (SPS > 1 and pc >= g["PP"]) else 0
                             p = pc - sub * g["PP"]
                             j = j0 + sub
@@ -162,14 +167,13 @@ def check_conv3x3i(W, N, emit=None):
                                 emit.setdefault((b, wv), []).append(
                                     (s_idx % 2 * g["SLOT"] + dst,
                                      np.where(s_ok, code(KX, src[us] + j * 32), code(KZ, (lane & 3) * 16 + j * 32))))
-                        elif pc < g["PPS"] + g["WPS"]:
-                            wp = pc - g["PPS"]
+                        elif wp is not None and wp < g["WPS"]:
                             sub = 1 if (SPS > 1 and wp >= g["WP"]) else 0
                             q = wp - sub * g["WP"]
                             s0 = wbase + (j0 + sub) * 128 * g["IPITCH"] + q * 1024
                             need(s0 >= 0 and s0 + 1024 <= wbytes, "weight piece past the packed image")
                             need(sub * g["WB"] + q * 1024 + 1024 <= g["WBS"], "weight piece past the weight region")
-                            issued[pc] += 1
+                            issued[g["PPS"] + wp] += 1
                             if emit is not None:
                                 emit.setdefault((b, wv), []).append(
                                     (s_idx % 2 * g["SLOT"] + wp * 1024, code(KW, s0 + 16 * lane)))
@@ -261,8 +265,11 @@ def check_s2i(OW, N, emit=None):
     n_ot = OC // g["JOT"]
     NI = n_ot * ((P + g["JL"] - 1) // g["JL"])
     Gd = min(NI, NCU)
-    DPW = (g["NPIECE"] + JNW - 1) // JNW
-    KP = (g["PP"] + JNW - 1) // JNW
+    # s2i_body: patch slots k < KPP (piece wv + 8 k), then weight slots
+    # (weight piece wv + 8 (k - KPP)); empty slots are issued masked
+    KPP = (g["PP"] + JNW - 1) // JNW
+    KPW = (g["WPC"] + JNW - 1) // JNW
+    DPW = KPP + KPW
     WCP = g["WB"] // 1024
     lds_total = g["OFF_AB"] + 4 * OC * 4
     need(lds_total <= 160 * 1024, "LDS budget")
@@ -317,8 +324,9 @@ def check_s2i(OW, N, emit=None):
                 issued = np.zeros(g["NPIECE"], int)
                 for wv in range(JNW):
                     for k in range(DPW):
-                        pc = wv + k * JNW
-                        if k < KP and pc < g["PP"]:
+                        pc = wv + k * JNW if k < KPP else None
+                        wp = wv + (k - KPP) * JNW if k >= KPP else None
+                        if pc is not None and pc < g["PP"]:
                             us = pc * 64 + lane
                             s_ok = src[us] >= 0
                             need(src[us][s_ok] + j * 32 + 16 <= xbytes, "patch source past the input")
@@ -329,8 +337,7 @@ def check_s2i(OW, N, emit=None):
                                 emit.setdefault((b, wv), []).append(
                                     (s_idx % 2 * g["SLOT"] + g["OFF_P"] + pc * 1024,
                                      np.where(s_ok, code(KX, src[us] + j * 32), code(KZ, (lane & 3) * 16 + j * 32))))
-                        elif pc < g["PP"] + g["WPC"]:
-                            wp = pc - g["PP"]
+                        elif wp is not None and wp < g["WPC"]:
                             if wp < WCP:
                                 s0 = ot * NS * g["WB"] + j * g["WB"] + wp * 1024
                                 need(s0 + 1024 <= wbytes_c, "conv weight piece past the image")
@@ -338,7 +345,7 @@ def check_s2i(OW, N, emit=None):
                                 s0 = ot * NS * g["DB"] + j * g["DB"] + (wp - WCP) * 1024
                                 need(s0 + 1024 <= wbytes_d, "ds weight piece past the image")
                             need(wp * 1024 + 1024 <= g["OFF_P"], "weight piece into the patch region")
-                            issued[pc] += 1
+                            issued[g["PP"] + wp] += 1
                             if emit is not None:
                                 emit.setdefault((b, wv), []).append(
                                     (s_idx % 2 * g["SLOT"] + wp * 1024, code(KW if wp < WCP else KD, s0 + 16 * lane)))

@@ -15,11 +15,6 @@
 #include <cstdint>
 #include <vector>
 
-namespace dlq {
-#if PLANCAP_KIND == 0  // (one definition across the two objects)
-int packed_oc(int OC) { return OC <= 64 ? 64 : (OC + 127) / 128 * 128; }
-#endif
-}  // namespace dlq
 #if PLANCAP_KIND == 0
 #include "../../dlq_amd/csrc/conv3x3i.hip"
 #else
@@ -40,14 +35,16 @@ hipError_t dmalloc(T** p, size_t bytes) {
 // wave w of the launch (grid * 8 waves): cnt[w] pieces (at most max_rec),
 // lds[w * max_rec + i], src[(w * max_rec + i) * 64 + lane]; bases = the
 // device addresses of x, the conv weights, the downsample weights and the
-// kernel's zero block.  Returns the number of waves, or -1 on a HIP error.
+// kernel's zero block.  Returns the number of waves, -1 on a HIP error, or -2
+// if any piece went unrecorded (a wave past the buffers or past max_rec), -3
+// if the launch has more waves than the caller's arrays (max_waves) hold.
 #if PLANCAP_KIND == 0
 #define PLANCAP_RUN plancap_run_wide
 #else
 #define PLANCAP_RUN plancap_run_s2i
 #endif
 extern "C" int PLANCAP_RUN(int kind, int W, int N, unsigned max_rec, unsigned* cnt, unsigned* lds,
-                           unsigned long long* src, unsigned long long* bases) {
+                           unsigned long long* src, unsigned long long* bases, int max_waves) {
   if (kind != PLANCAP_KIND) return -1;
   const int C = kind == 0 ? (W == 28 ? 128 : W == 14 ? 256 : 512) : (W == 56 ? 64 : W == 28 ? 128 : 256);
   const int OW = kind == 0 ? W : W / 2, OC = kind == 0 ? C : 2 * C, P = N * OW * OW;
@@ -59,7 +56,14 @@ extern "C" int PLANCAP_RUN(int kind, int W, int N, unsigned max_rec, unsigned* c
   PlanPiece* buf = nullptr;
   unsigned* dcnt = nullptr;
   const int items = kind == 0 ? (OC / (OW == 7 ? 64 : 128)) * ((P + 391) / 392) : (OC / 128) * ((P + 195) / 196);
-  const int grid = items < 256 ? items : 256, nw = grid * 8;
+  // the launchers' grid: min(items, CUs) (num_cus_i / num_cus_s2i)
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+    ncu = 256;
+  const int grid = items < ncu ? items : ncu, nw = grid * 8;
+  const unsigned nwu = (unsigned)nw, zero_u = 0;
+  if (nw > max_waves) return -3;  // the caller's cnt / lds / src arrays hold max_waves waves
   if (dmalloc(&x, xb) || dmalloc(&w, wb) || dmalloc(&wd, db) || dmalloc(&y, yb) || dmalloc(&yd, yb) ||
       dmalloc(&ab, (size_t)4 * OC * 4) || dmalloc(&buf, (size_t)nw * max_rec * sizeof(PlanPiece)) ||
       dmalloc(&dcnt, (size_t)nw * 4))
@@ -67,7 +71,9 @@ extern "C" int PLANCAP_RUN(int kind, int W, int N, unsigned max_rec, unsigned* c
   if (hipMemset(dcnt, 0, (size_t)nw * 4) || hipMemset(ab, 0, (size_t)4 * OC * 4)) return -1;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_cap_buf), &buf, sizeof(buf)) ||
       hipMemcpyToSymbol(HIP_SYMBOL(g_cap_cnt), &dcnt, sizeof(dcnt)) ||
-      hipMemcpyToSymbol(HIP_SYMBOL(g_cap_max), &max_rec, sizeof(max_rec)))
+      hipMemcpyToSymbol(HIP_SYMBOL(g_cap_max), &max_rec, sizeof(max_rec)) ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_cap_nw), &nwu, sizeof(nwu)) ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_cap_drop), &zero_u, sizeof(zero_u)))
     return -1;
   ConvArgs a{};
   a.x = x;
@@ -97,6 +103,9 @@ extern "C" int PLANCAP_RUN(int kind, int W, int N, unsigned max_rec, unsigned* c
   if (e == hipSuccess) e = hipGetSymbolAddress(&zero, HIP_SYMBOL(g_zero_s2i));
 #endif
   if (e != hipSuccess || hipDeviceSynchronize() != hipSuccess) return -1;
+  unsigned dropped = 0;
+  if (hipMemcpyFromSymbol(&dropped, HIP_SYMBOL(g_cap_drop), sizeof(dropped)) != hipSuccess) return -1;
+  if (dropped) return -2;  // a piece went unrecorded: the comparison would be incomplete
   std::vector<PlanPiece> h((size_t)nw * max_rec);
   if (hipMemcpy(h.data(), buf, h.size() * sizeof(PlanPiece), hipMemcpyDeviceToHost) ||
       hipMemcpy(cnt, dcnt, (size_t)nw * 4, hipMemcpyDeviceToHost))

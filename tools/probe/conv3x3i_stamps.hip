@@ -1,16 +1,13 @@
 // Timing probe (not product code): per-wave s_memtime stamps of the 392-px
 // wide stride-1 conv kernel (conv3x3i.hip), random int8 data; argv: W, dbg
 // bits (2 no LDS-DMA, 4 no epilogue, 8 B fragments read for the first k-steps
-// only), N.
+// only), N, residual (0 = none; default on).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DDLQ_STAMPS \
 //          -I dlq_amd/csrc tools/probe/conv3x3i_stamps.hip -o tools/probe/conv3x3i_stamps
 #define DLQ_ABLATION 1  // the kernel honours a.dbg (timing ablations)
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
-namespace dlq {
-int packed_oc(int OC) { return OC <= 64 ? 64 : (OC + 127) / 128 * 128; }
-}
 #include "../../dlq_amd/csrc/conv3x3i.hip"
 
 using namespace dlq;
@@ -36,7 +33,7 @@ int main(int argc, char** argv) {
   std::vector<float> hal(C, 1e-4f);
   if (hipMemcpy(al, hal.data(), C * 4, hipMemcpyHostToDevice) || hipMemset(be, 0, C * 4)) return 3;
   ConvArgs a{};
-  a.x = x; a.w = w; a.alpha = al; a.beta = be; a.res = res; a.y = y; a.s_res = 0.01f;
+  a.x = x; a.w = w; a.alpha = al; a.beta = be; a.res = (argc > 4 && atoi(argv[4]) == 0) ? nullptr : res; a.y = y; a.s_res = 0.01f;
   a.N = N; a.H = W; a.W = W; a.C = C; a.OH = W; a.OW = W; a.OC = C; a.OCp = C; a.K = 9 * C;
   a.kH = a.kW = 3; a.sH = a.sW = 1; a.pH = a.pW = 1; a.P = P; a.relu = 1; a.out_kind = 0; a.dbg = dbg;
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);

@@ -11,9 +11,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
-namespace dlq {
-int packed_oc(int OC) { return OC <= 64 ? 64 : (OC + 127) / 128 * 128; }
-}
 #include "../../dlq_amd/csrc/conv3x3s2i.hip"
 
 using namespace dlq;

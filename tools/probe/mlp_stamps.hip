@@ -6,9 +6,6 @@
 #include <algorithm>
 #include <cstdio>
 #include <vector>
-namespace dlq {
-int packed_oc(int OC) { return OC <= 64 ? 64 : (OC + 127) / 128 * 128; }
-}
 #include "../../dlq_amd/csrc/head.hip"
 using namespace dlq;
 int main() {
