@@ -298,9 +298,85 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
   // one stage (s < nst); MORE: a stage follows (its DMA is issued in this
   // one).  int8: every stage but the last, and the last, as two
   // instantiations, so no DMA issue sits behind a runtime branch.
+  // The epilogues of the item (ot, p0): conv1 (+ downsample), from acc / accd.
+  auto item_epilogue = [&](int ot, int p0) {
+    if constexpr (OUT == 2) {
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int e = perm_at<OW>((f0 + f) * 32 + lr), p = p0 + (e & 0x3fff);
+        const bool keep = !(e & 0x4000) && p < a.P;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int oc = ot * JOT + mt * 32 + 8 * g + 4 * lh;
+          v4i* dst = keep ? (v4i*)((int*)a.y + (size_t)p * a.OC + oc) : (v4i*)(g_trash_s2i + lane * 16);
+          if constexpr (F8)  // raw fp32 accumulators
+            *dst = v4i{__float_as_int(acc[f][4 * g]), __float_as_int(acc[f][4 * g + 1]),
+                       __float_as_int(acc[f][4 * g + 2]), __float_as_int(acc[f][4 * g + 3])};
+          else
+            *dst = v4i{acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
+        }
+      }
+    } else {
+      // probe builds: dbg 16 / 32 send the downsample / conv1 stores to the trash line
+      auto epi = [&](const Acc* ac, int ab_off, float lo, int8_t* out, auto rc, bool no_store) {
+        constexpr bool RL = decltype(rc)::value;
+        float al[4][4], be[4][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int oc = ot * JOT + mt * 32 + 8 * g + 4 * lh;
+          const v4i a4 = *(const v4i*)(lds + G::OFF_AB + ab_off + oc * 4);
+          const v4i b4 = *(const v4i*)(lds + G::OFF_AB + ab_off + (OC + oc) * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            al[g][e] = __int_as_float(a4[e]);
+            be[g][e] = __int_as_float(b4[e]);
+          }
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          unsigned q[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            if constexpr (F8) {
+              const float a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
+              q[g] = epi4_f8(a4, al[g], be[g], lo);
+            } else if constexpr (RL) {
+              const int a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
+              q[g] = epi4_relu(a4, al[g], be[g]);
+            } else {
+              const int a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
+              q[g] = epi4(a4, al[g], be[g], lo);
+            }
+          }
+          swap32(q[0], q[2]);
+          swap32(q[1], q[3]);
+          const int e = perm_at<OW>((f0 + f) * 32 + lr), p = p0 + (e & 0x3fff);
+          const bool keep = !(e & 0x4000) && p < a.P && !no_store;
+          v4i* dst = keep ? (v4i*)(out + (size_t)p * a.OC + ot * JOT + mt * 32 + lh * 16)
+                          : (v4i*)(g_trash_s2i + lane * 16);
+          if (DLQ_ABL(a, 128))  // probe builds: one contiguous KiB per wave-store (store-pattern ablation)
+            dst = (v4i*)(out + ((((size_t)blockIdx.x * JNW + wave) * 64 + (size_t)(p0 / JL) * 8 + f) * 1024) %
+                                   ((size_t)a.P * a.OC) + lane * 16);
+          if (!DLQ_ABL(a, 64))  // probe builds: dbg 64 drops the int8 stores
+            *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
+        }
+      };
+      constexpr float LO = F8 ? -448.f : -127.f;
+      epi(acc, 0, a.relu ? 0.f : LO, (int8_t*)a.y, std::integral_constant<bool, RELU && !F8>{}, DLQ_ABL(a, 32));
+      if constexpr (DS) {  // probe builds: dbg 8 skips the downsample's epilogue
+        if (!DLQ_ABL(a, 8)) epi(accd, 2 * OC * 4, LO, y_ds, std::integral_constant<bool, false>{}, DLQ_ABL(a, 16));
+      }
+    }
+  };
+
+  // one stage (s < nst); MORE: a stage follows (its DMA is issued in this
+  // one).  int8: every stage but the last, and the last, as two
+  // instantiations, so no DMA issue sits behind a runtime branch.
   auto stage = [&](int s, auto more_c) {
     const int li = s / NS, j = s - li * NS;
     if (s == 0) JSTAMP(58);
+    // Stage s has landed once every older VM op is done except the previous
+    // item's epilogue stores (issued after this stage's DMA).
     if (j == 0 && s > 0)
       wait_vm_const<STORES>();
     else
@@ -431,76 +507,10 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     }  // int8 MFMA loop
 
     JSTAMP(2 + 2 * s);
-    if (j != NS - 1 || DLQ_ABL(a, 4)) return;  // probe builds: timing without the epilogues
-    // ---- fused epilogues of the item ----
-    if constexpr (OUT == 2) {
-#pragma unroll
-      for (int f = 0; f < NF; ++f) {
-        const int e = perm_at<OW>((f0 + f) * 32 + lr), p = cur_p0 + (e & 0x3fff);
-        const bool keep = !(e & 0x4000) && p < a.P;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int oc = cur_ot * JOT + mt * 32 + 8 * g + 4 * lh;
-          v4i* dst = keep ? (v4i*)((int*)a.y + (size_t)p * a.OC + oc) : (v4i*)(g_trash_s2i + lane * 16);
-          if constexpr (F8)  // raw fp32 accumulators
-            *dst = v4i{__float_as_int(acc[f][4 * g]), __float_as_int(acc[f][4 * g + 1]),
-                       __float_as_int(acc[f][4 * g + 2]), __float_as_int(acc[f][4 * g + 3])};
-          else
-            *dst = v4i{acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
-        }
-      }
-    } else {
-      // probe builds: dbg 16 / 32 send the downsample / conv1 stores to the trash line
-      auto epi = [&](const Acc* ac, int ab_off, float lo, int8_t* out, auto rc, bool no_store) {
-        constexpr bool RL = decltype(rc)::value;
-        float al[4][4], be[4][4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int oc = cur_ot * JOT + mt * 32 + 8 * g + 4 * lh;
-          const v4i a4 = *(const v4i*)(lds + G::OFF_AB + ab_off + oc * 4);
-          const v4i b4 = *(const v4i*)(lds + G::OFF_AB + ab_off + (OC + oc) * 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            al[g][e] = __int_as_float(a4[e]);
-            be[g][e] = __int_as_float(b4[e]);
-          }
-        }
-#pragma unroll
-        for (int f = 0; f < NF; ++f) {
-          unsigned q[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            if constexpr (F8) {
-              const float a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
-              q[g] = epi4_f8(a4, al[g], be[g], lo);
-            } else if constexpr (RL) {
-              const int a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
-              q[g] = epi4_relu(a4, al[g], be[g]);
-            } else {
-              const int a4[4] = {ac[f][4 * g], ac[f][4 * g + 1], ac[f][4 * g + 2], ac[f][4 * g + 3]};
-              q[g] = epi4(a4, al[g], be[g], lo);
-            }
-          }
-          swap32(q[0], q[2]);
-          swap32(q[1], q[3]);
-          const int e = perm_at<OW>((f0 + f) * 32 + lr), p = cur_p0 + (e & 0x3fff);
-          const bool keep = !(e & 0x4000) && p < a.P && !no_store;
-          v4i* dst = keep ? (v4i*)(out + (size_t)p * a.OC + cur_ot * JOT + mt * 32 + lh * 16)
-                          : (v4i*)(g_trash_s2i + lane * 16);
-          if (DLQ_ABL(a, 128))  // probe builds: one contiguous KiB per wave-store (store-pattern ablation)
-            dst = (v4i*)(out + ((((size_t)blockIdx.x * JNW + wave) * 64 + (size_t)(cur_p0 / JL) * 8 + f) * 1024) %
-                                   ((size_t)a.P * a.OC) + lane * 16);
-          if (!DLQ_ABL(a, 64))  // probe builds: dbg 64 drops the int8 stores
-            *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
-        }
-      };
-      constexpr float LO = F8 ? -448.f : -127.f;
-      epi(acc, 0, a.relu ? 0.f : LO, (int8_t*)a.y, std::integral_constant<bool, RELU && !F8>{}, DLQ_ABL(a, 32));
-      if constexpr (DS) {  // probe builds: dbg 8 skips the downsample's epilogue
-        if (!DLQ_ABL(a, 8)) epi(accd, 2 * OC * 4, LO, y_ds, std::integral_constant<bool, false>{}, DLQ_ABL(a, 16));
-      }
-    }
-    };
+    if (j != NS - 1) return;
+    if (DLQ_ABL(a, 4)) return;  // probe builds: timing without the epilogues
+    item_epilogue(cur_ot, cur_p0);
+  };
   if constexpr (F8) {
     for (int s = 0; s < nst; ++s) stage(s, std::true_type{});
   } else {
