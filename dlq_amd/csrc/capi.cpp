@@ -124,6 +124,9 @@ std::atomic<int> g_knob_l1_grid{env_int("DLQ_L1_GRID")};
 std::atomic<int> g_knob_head_split{env_int("DLQ_HEAD_SPLIT")};
 std::atomic<int> g_knob_graph{env_int("DLQ_GRAPH")};
 std::atomic<int> g_knob_gemm_tile{env_int("DLQ_GEMM_TILE")};
+// bumped by every dlq_set_knob: a forward captured as a hipGraph under other
+// knob values (head_split, l1_grid change its launches) is captured again
+std::atomic<unsigned> g_knob_gen{0};
 
 namespace {
 std::atomic<int>* knob(const char* name) {
@@ -146,6 +149,7 @@ int dlq_set_knob(const char* name, int value) {
   std::atomic<int>* k = knob(name);
   if (!k) return fail(DLQ_ERR_ARG, "set_knob: unknown knob");
   k->store(value);
+  g_knob_gen.fetch_add(1);
   return DLQ_OK;
 }
 

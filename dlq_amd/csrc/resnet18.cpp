@@ -107,6 +107,7 @@ struct dlq_resnet18 {
   // x, logits) are baked in, so prepare / precision changes drop it.
   hipStream_t gs = nullptr;
   hipGraphExec_t gexec = nullptr;
+  unsigned g_gen = 0;  // g_knob_gen at capture
   const float* g_x = nullptr;
   float* g_logits = nullptr;
   int g_B = 0;
@@ -977,7 +978,8 @@ bool use_graph(const dlq_resnet18* m) {
 
 int forward_graph(dlq_resnet18* m, const float* x, int B, float* logits, hipStream_t s) {
   hipError_t e = hipSuccess;
-  if (!m->gexec || m->g_x != x || m->g_B != B || m->g_logits != logits) {
+  const unsigned gen = g_knob_gen.load(std::memory_order_relaxed);
+  if (!m->gexec || m->g_x != x || m->g_B != B || m->g_logits != logits || m->g_gen != gen) {
     drop_graph(m);
     if (!m->gs && (e = hipStreamCreateWithFlags(&m->gs, hipStreamNonBlocking)) != hipSuccess)
       return hip_fail(e, "graph stream");
@@ -998,6 +1000,7 @@ int forward_graph(dlq_resnet18* m, const float* x, int B, float* logits, hipStre
       return hip_fail(e, "hipGraphInstantiate");
     }
     m->g_x = x;
+    m->g_gen = gen;
     m->g_B = B;
     m->g_logits = logits;
   }
