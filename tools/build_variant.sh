@@ -1,16 +1,19 @@
 #!/bin/bash
 # Build a variant of libdlq.so for A/B timing (tools/ab.py):
 #   tools/build_variant.sh NAME "-DFLAG=1 ..."
-# -> scratch/NAME/libdlq_ab.so (scratch/ is git-ignored; it travels to the GPU
-# box; not named libdlq.so so it is never mistaken for the product library).
+# -> abvar/NAME/libdlq_ab.so (git-ignored but not gpurun-ignored, so it travels
+# to the GPU box for tools/ab.py; delete abvar/ once the A/B is recorded so no
+# stale library rides along; not named libdlq.so so it is never mistaken for
+# the product library).  Objects go to scratch/ (gpurun-ignored).
 # SRC=dir builds the sources of another tree (default dlq_amd/csrc).
 set -e
 cd "$(dirname "$0")/.."
 NAME=$1
 shift
 FLAGS="$*"
-OUT=scratch/$NAME
-mkdir -p $OUT/obj
+OUT=abvar/$NAME
+OBJ=scratch/abobj/$NAME
+mkdir -p $OUT $OBJ
 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result $FLAGS"
 pids=()
 objs=()
@@ -18,7 +21,7 @@ SRC=${SRC:-dlq_amd/csrc}
 for f in $SRC/*.hip $SRC/*.cpp; do
   b=$(basename $f)
   [ "$b" = main_e2e.cpp ] || [ "$b" = main_step.cpp ] && continue
-  o=$OUT/obj/${b%.*}.o
+  o=$OBJ/${b%.*}.o
   objs+=($o)
   if [[ $f == *.cpp ]]; then x="-x hip"; else x=""; fi
   # as the Makefile (block_l1.hip), plus any file named in $NOSLP
