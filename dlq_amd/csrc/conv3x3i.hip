@@ -60,15 +60,6 @@ constexpr int IL = 392;        // output pixels per item
 constexpr int ISC = 32;        // input channels per stage
 constexpr int IPITCH = 9 * ISC + 16;  // weight row pitch (304 B, odd multiple of 16: conflict-free)
 constexpr int INW = 8;         // waves per workgroup
-#ifndef DLQ_GMIN
-#define DLQ_GMIN 0  // A/B builds: group only the bodies with at least this many tiles
-#endif
-#ifndef DLQ_EPIVALU
-#define DLQ_EPIVALU 1
-#endif
-#ifndef DLQ_UNGROUPED
-#define DLQ_UNGROUPED 0        // A/B builds: 1 = every item's epilogue after its last MFMA (no grouped last stage)
-#endif
 
 // SPS: 32-channel slices per stage.  The 7x7 launches (C = 512: sixteen
 // one-slice stages of 58.5 MFMAs per SIMD) take two slices per stage, which
@@ -282,8 +273,6 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   // fragments only one tap (6 MFMAs) ahead, waited on LDS latency there;
   // the 7-tile waves have no registers to spare for a second set
   constexpr bool PF2 = NF <= 6;
-  // int8 requantising launches end every item with the grouped stage below
-  constexpr bool GROUPED = !F8 && OUT == 0 && !DLQ_UNGROUPED && NF >= DLQ_GMIN;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int lr = lane & 31, lh = lane >> 5;
@@ -317,59 +306,6 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   v4i rq[NF];
   int cur_ot = 0, cur_p0 = 0;
 
-  // the output as a buffer resource (P * OC < 2^31 bytes: launch_ci)
-  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, a.P * a.OC, 0x00020000);
-
-  // One tile's fused epilogue (int8, OUT == 0): residual (awaited: every VM
-  // op younger than it is one of the later tiles' residual loads or an
-  // earlier tile's store, NF - 1 in all), requantisation, two permlane32
-  // swaps into the store layout, one 16-byte store per lane.
-  auto epi_tile = [&](auto f, auto vmc) __attribute__((always_inline)) {  // generic: instantiated only where called (int8 OUT 0)
-    unsigned r[4] = {0, 0, 0, 0};
-    if constexpr (RES) {
-      asm volatile("s_waitcnt vmcnt(%1)" : "+v"(rq[f]) : "n"(decltype(vmc)::value) : "memory");
-      r[0] = (unsigned)rq[f][0];
-      r[1] = (unsigned)rq[f][1];
-      r[2] = (unsigned)rq[f][2];
-      r[3] = (unsigned)rq[f][3];
-      swap32(r[0], r[1]);
-      swap32(r[2], r[3]);
-    }
-    const unsigned rg[4] = {r[0], r[2], r[1], r[3]};
-    const float lo = a.relu ? 0.f : -127.f;
-    unsigned q[4];
-    // alpha / beta re-read per tile (an opaque address: hoisted, they would
-    // hold 32 registers through the grouped stage)
-    int ab_off = OFF_AB + (cur_ot * G::OT + mt * 32 + 4 * lh) * 4;
-    asm volatile("" : "+v"(ab_off));
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const v4i a4 = *(const v4i*)(lds + ab_off + 32 * g);
-      const v4i b4 = *(const v4i*)(lds + ab_off + 32 * g + C * 4);
-      const float al[4] = {__int_as_float(a4[0]), __int_as_float(a4[1]), __int_as_float(a4[2]), __int_as_float(a4[3])};
-      const float be[4] = {__int_as_float(b4[0]), __int_as_float(b4[1]), __int_as_float(b4[2]), __int_as_float(b4[3])};
-      const int ac[4] = {acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
-      if constexpr (RELU && RES)
-        q[g] = epi4_res_relu(ac, al, be, rg[g], a.s_res);
-      else if constexpr (RELU)
-        q[g] = epi4_relu(ac, al, be);
-      else if constexpr (RES)
-        q[g] = epi4_res(ac, al, be, rg[g], a.s_res, lo);
-      else
-        q[g] = epi4(ac, al, be, lo);
-    }
-    swap32(q[0], q[2]);
-    swap32(q[1], q[3]);
-    // a buffer store: pixels past the item or the batch get an offset past
-    // the buffer's size, which the hardware drops (a select, no branch: a
-    // branch here would split group B's MFMA region)
-    const int lp = (f0 + f) * 32 + lr, p = cur_p0 + lp;
-    const bool keep = lp < IL && p < a.P;
-    const int off = keep ? p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16 : 0x7ffffff0;
-    if (!DLQ_ABL(a, 64))  // probe builds: dbg 64 drops the int8 stores
-      __builtin_amdgcn_raw_buffer_store_b128(v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]}, yrs, off, 0, 0);
-  };
-
   ISTAMP(0);
   if (loader) {
     prep_for(0);
@@ -381,10 +317,8 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   // one stage (s < nst); MORE: a stage follows (its DMA is issued in this
   // one).  Two instantiations -- every stage but the last, and the last --
   // so no DMA issue sits behind a runtime branch.
-  auto stage = [&](int s, auto more_c, auto grp_c) __attribute__((always_inline)) {
-    constexpr bool GRP = decltype(grp_c)::value;  // grouped tile order (int8 requantising launches)
+  auto stage = [&](int s, auto more_c) {
     const int li = s / NS, j = s - li * NS;
-    const bool last = j == NS - 1;  // the item's last stage: its epilogue runs in this one
     // Stage s has landed once every older VM op is done except the previous
     // item's epilogue stores (issued after this stage's DMA).
     if (j == 0 && s > 0)
@@ -394,7 +328,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     __builtin_amdgcn_s_barrier();
     ISTAMP(1 + 2 * s);
     // (fp8: one instantiation with the runtime test -- two spill its registers)
-    const bool more = decltype(more_c)::value && ((!F8 && !GRP) || s + 1 < nst);
+    const bool more = decltype(more_c)::value && (!F8 || s + 1 < nst);
     if (more && loader) prep_for(s + 1);
 
     if (j == 0) {
@@ -473,109 +407,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       const size_t off = keep ? (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16 : 0;
       rq[f] = gload16_untracked(a.res + off);
     };
-    if constexpr (GRP) {
-    // Grouped tile order: the tiles in two groups, [0, NA) then [NA, NF),
-    // each through all k-steps of the stage.  In an item's last stage group
-    // A's accumulators are final while group B's MFMAs still run, and group
-    // A's epilogue is interleaved with them (its VALU beside this wave's and
-    // the partner wave's MFMAs, a uniform branch per slice); only group B's
-    // requantisation is left after the last MFMA.  The next stage's DMA goes
-    // out in group A's first k-steps, two pieces per k-step; then (last
-    // stage) the residual loads of group A; group B's follow group A's last
-    // epilogue (their registers would not fit beside the pass): VM order
-    // DMA pieces, residuals of A, A's stores, residuals of B, B's stores, so
-    // the wait for a tile's residual is vmcnt(NA - 1) in group A, vmcnt(NB -
-    // 1) in group B.  (The last stage as a separate instantiation beside the
-    // other stages' body spilled hundreds of registers.)
-    constexpr int NA = (NF + 1) / 2, NB = NF - NA;
-    constexpr int KD = (DPW + 1) / 2;  // k-steps that carry DMA pieces
-    static_assert(KD < KSN, "the residual loads follow the DMA pieces inside group A's pass");
-    auto run_group = [&](auto g0c, auto gnc, auto epic) __attribute__((always_inline)) {
-      constexpr int G0 = decltype(g0c)::value, GN = decltype(gnc)::value;
-      constexpr bool EPI = decltype(epic)::value;  // group B's pass: group A's epilogue between its MFMAs
-      v4i fa[2], fb[2][GN];
-      auto ld_b = [&](int ks, int f) { fb[ks & 1][f] = *(const v4i*)(lds + b_off(ks, G0 + f)); };
-      fa[0] = a_at(0);
-#pragma unroll
-      for (int f = 0; f < GN; ++f) ld_b(0, f);
-      fa[1] = a_at(1);
-#pragma unroll
-      for (int f = 0; f < GN; ++f) ld_b(1, f);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ks = 0; ks < KSN; ++ks) {
-        const int bu = ks & 1;
-        const int k0 = EPI || ks >= KD ? DPW : 2 * ks, k1 = EPI || ks >= KD ? DPW : (2 * ks + 2 < DPW ? 2 * ks + 2 : DPW);
-        if (dma) {
-#pragma unroll
-          for (int k = k0; k < k1; ++k) issue_piece(s + 1, k);
-        }
-#pragma unroll
-        for (int f = 0; f < GN; ++f) {
-          acc[G0 + f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu], fb[bu][f], acc[G0 + f], 0, 0, 0);
-          if (f == GN - 1 && ks + 2 < KSN) fa[bu] = a_at(ks + 2);
-          if (ks + 2 < KSN) ld_b(ks + 2, f);
-        }
-        if constexpr (OUT == 0 && RES && !EPI) {
-          if (last && ks == KD) {
-#pragma unroll
-            for (int f = 0; f < NA; ++f) res_load(f);
-          }
-        }
-        if constexpr (EPI) {
-#pragma unroll
-          for (int t = 0; t < NA; ++t)
-            if (last && ks == (t + 1) * KSN / (NA + 1)) {
-              epi_tile(t, std::integral_constant<int, NA - 1>{});
-              if constexpr (OUT == 0 && RES) {
-                if (t == NA - 1) {
-#pragma unroll
-                  for (int f = NA; f < NF; ++f) res_load(f);
-                }
-              }
-            }
-        }
-        const int i0 = GN > 1 ? 1 : 0, nvm0 = (k1 > k0) + (k1 > k0 + 1 && i0 == GN - 1), nvm1 = k1 > k0 + 1 && i0 != GN - 1;
-        if (ks + 2 < KSN) {
-#pragma unroll
-          for (int i = 0; i < GN; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-            if (i == GN - 1)
-              __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read (B + the A two k-steps ahead)
-            else
-              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read (B)
-            const int nv = (i == i0 ? nvm0 : 0) + (i == GN - 1 ? nvm1 : 0);
-            if (nv == 1) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (LDS-DMA)
-            if (nv == 2) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
-            if (EPI && DLQ_EPIVALU) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // VALU (group A's epilogue)
-          }
-        } else {
-          if (k1 == k0 + 1) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-          if (k1 == k0 + 2) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
-#pragma unroll
-          for (int i = 0; i < GN; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            if (EPI && DLQ_EPIVALU) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
-          }
-        }
-        // one scheduling region per k-step: an epilogue slice stays beside
-        // the MFMAs it was placed with (left to one region, the scheduler
-        // hoisted every tile's conversions and spilled)
-        if (EPI) __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    using IA = std::integral_constant<int, NA>;
-    using IB = std::integral_constant<int, NB>;
-    run_group(std::integral_constant<int, 0>{}, IA{}, std::false_type{});
-    __builtin_amdgcn_sched_barrier(0);
-    run_group(IA{}, IB{}, std::true_type{});
-    __builtin_amdgcn_sched_barrier(0);
-    ISTAMP(2 + 2 * s);
-    if (!last || DLQ_ABL(a, 4)) return;
-#pragma unroll
-    for (int t = NA; t < NF; ++t) epi_tile(t, std::integral_constant<int, NB - 1>{});
-    return;
-    } else if constexpr (PF2) {
+    if constexpr (PF2) {
     // B fragments two k-steps ahead: fb[ks & 1][f] holds k-step ks of tile f
     // and is re-loaded with ks + 2 right after the MFMA that consumed it (the
     // LDS latency then has two k-steps of the SIMD's MFMAs to hide in, enough
@@ -673,7 +505,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     }  // int8 MFMA loop
 
     ISTAMP(2 + 2 * s);
-    if (GROUPED || j != NS - 1 || DLQ_ABL(a, 4)) return;  // probe builds: timing without the epilogue
+    if (j != NS - 1 || DLQ_ABL(a, 4)) return;  // probe builds: timing without the epilogue
     // ---- fused epilogue of the item ----
     if constexpr (OUT == 2) {
 #pragma unroll
@@ -757,18 +589,10 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     }
     };
   if constexpr (F8) {
-    for (int s = 0; s < nst; ++s) stage(s, std::true_type{}, std::false_type{});
-  } else if constexpr (GROUPED) {
-    int s = 0;
-    for (int li = 0; li < st.nit; ++li) {
-#pragma nounroll
-      for (int j = 0; j + 1 < NS; ++j, ++s) stage(s, std::true_type{}, std::false_type{});
-      stage(s, std::true_type{}, std::true_type{});
-      ++s;
-    }
+    for (int s = 0; s < nst; ++s) stage(s, std::true_type{});
   } else {
-    for (int s = 0; s + 1 < nst; ++s) stage(s, std::true_type{}, std::false_type{});
-    if (nst > 0) stage(nst - 1, std::false_type{}, std::false_type{});
+    for (int s = 0; s + 1 < nst; ++s) stage(s, std::true_type{});
+    if (nst > 0) stage(nst - 1, std::false_type{});
   }
   ISTAMP(62);
   wait_vm0();
