@@ -312,6 +312,16 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #pragma unroll
     for (int k = 0; k < DPW; ++k) issue_piece(0, k);
   }
+  if (DLQ_ABL(a, 256)) {  // probe builds: stage 0 landed from a cold L2, then the same pieces again (L2-hot)
+    wait_vm_const<0>();
+    __builtin_amdgcn_s_barrier();
+    ISTAMP(60);
+#pragma unroll
+    for (int k = 0; k < DPW; ++k) issue_piece(0, k);
+    wait_vm_const<0>();
+    __builtin_amdgcn_s_barrier();
+    ISTAMP(61);
+  }
   conv3x3i_init<W, C, OUT, SPS>(a, lds);
 
   // one stage (s < nst); MORE: a stage follows (its DMA is issued in this

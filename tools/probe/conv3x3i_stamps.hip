@@ -1,7 +1,7 @@
 // Timing probe (not product code): per-wave s_memtime stamps of the 392-px
 // wide stride-1 conv kernel (conv3x3i.hip), random int8 data; argv: W, dbg
 // bits (2 no LDS-DMA, 4 no epilogue, 8 B fragments read for the first k-steps
-// only), N, residual (0 = none; default on).
+// only, 256 stage 0's DMA issued twice: cold, then L2-hot), N, residual (0 = none; default on).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DDLQ_STAMPS \
 //          -I dlq_amd/csrc tools/probe/conv3x3i_stamps.hip -o tools/probe/conv3x3i_stamps
 #define DLQ_ABLATION 1  // the kernel honours a.dbg (timing ablations)
@@ -50,14 +50,16 @@ int main(int argc, char** argv) {
 #ifdef DLQ_STAMPS
   std::vector<unsigned long long> st(256 * 8 * 64);
   hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_stamps_i), st.size() * 8);
-  const int NS = C / 32, nst = (W == 28 ? 2 : 1) * NS;
+  const int NS = C / 32 / (W == 7 ? 2 : 1), nst = (W == 28 ? 2 : 1) * NS;
   for (int blk : {0, 77, 200}) {
     for (int wv : {0, 4, 5}) {
       const unsigned long long* s = &st[(blk * 8 + wv) * 64];
       printf("blk %3d wave %d: pro %5llu |", blk, wv, s[1] - s[0]);
       for (int k = 0; k < nst; ++k)
         printf(" %llu/%llu", k ? s[1 + 2 * k] - s[2 * k] : 0ull, s[2 + 2 * k] - s[1 + 2 * k]);
-      printf(" | epi %llu drain %llu total %llu\n", s[62] - s[2 * nst], s[63] - s[62], s[63] - s[0]);
+      printf(" | epi %llu drain %llu total %llu", s[62] - s[2 * nst], s[63] - s[62], s[63] - s[0]);
+      if (dbg & 256) printf(" | stage-0 DMA cold %llu, again (L2-hot) %llu", s[60] - s[0], s[61] - s[60]);
+      printf("\n");
     }
   }
 #endif
