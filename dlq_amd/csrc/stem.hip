@@ -516,8 +516,8 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
 // a conv row are 4 contiguous bytes (kh, kh + 1): one ds_write_b32 per conv
 // row and channel where two lanes issued a ds_write_b16 each.  Same item
 // walk, ring, band logic, pooling and numerics as stem_fused_kernel:
-// 61.5-62.8 -> 59.2-60.6 us per launch (four A/B rounds, one box; -DDLQ_X_STEM1
-// launches the one-tile kernel), bit-identical.
+// 61.5-62.8 -> 59.2-60.6 us per launch (four A/B rounds, one box, round 4),
+// bit-identical.
 constexpr int S2W = 4;                          // waves: one per column quarter
 constexpr int STG2 = 64 * 16;                   // per wave: [64 oc][16 px] bytes
 constexpr int OFF_STAGE2 = OFF_CR + CR_SLOTS * CR_ROW;
