@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--extras", type=int, default=1,
                     help="1: also measure BASELINE configs[0], [1], [4] and the GEMM drop-in after the timed "
                          "region (rank 0, N = 1) and report them under extra_configs")
+    ap.add_argument("--cal-images", type=int, default=32,
+                    help="seeded synthetic images the activation scales are calibrated on (GPU fp32 reference "
+                         "forward, dlq_resnet18_calibrate; the last setup step before the warmup)")
     ap.add_argument("--precision", choices=("int8", "fp8"), default="int8",
                     help="int8 = the headline (configs[2]/[3]); fp8 = e4m3 activations + per-channel "
                          "e4m3 weights on the fp8 MFMA (configs[4])")
@@ -432,14 +435,20 @@ def main():
     from dlq_amd.lib import FAMILIES
     from dlq_amd.models import ResNet18Int8, resnet18_state_dict
     from dlq_amd.quant import calibrate_resnet18
-    from dlq_amd.models import synthetic_images
+    from dlq_amd.models import synthetic_images, site_names
 
     B = args.batch
     sd = resnet18_state_dict(SEED)
-    # Offline calibration on the CPU (deterministic, identical on every rank).
     fp8 = args.precision == "fp8"
-    scales = calibrate_resnet18(sd, synthetic_images(2, seed=SEED + 1), device="cpu", qmax=448.0 if fp8 else 127.0)
-    model = ResNet18Int8(sd, scales, max_batch=B, precision=args.precision)
+    qmax = 448.0 if fp8 else 127.0
+    if args.cal_images > 0:
+        # scales set below by the engine's GPU calibration; these only let the
+        # engine prepare once before it
+        model = ResNet18Int8(sd, {s: 1.0 for s in site_names()}, max_batch=max(B, args.cal_images),
+                             precision=args.precision)
+    else:  # the CPU path (torch fp32 forward on 2 images), for comparison
+        scales = calibrate_resnet18(sd, synthetic_images(2, seed=SEED + 1), device="cpu", qmax=qmax)
+        model = ResNet18Int8(sd, scales, max_batch=B, precision=args.precision)
     conv_macs, fc_macs = model.macs_per_image()
 
     # Synthetic NCHW input generated on the device (seeded per rank), resident in HBM.
@@ -464,6 +473,17 @@ def main():
         pipe = GatherPipeline(lambda xx, out: model.forward(xx, out), B, world, dev)
         logits = pipe.logits[0]
     fwd = lambda xx: model.forward(xx, logits)  # noqa: E731
+
+    if args.cal_images > 0:
+        # Activation scales from the engine's fp32 reference forward on the
+        # GPU (dlq_resnet18_calibrate: the reference's forward op for op,
+        # scale = amax / qmax per site, bit-identical to the oracle's) over
+        # seeded synthetic images: identical on every rank, ~70 ms on the
+        # GPU, and no rank spends its host threads on a torch calibration
+        # (eight ranks used to run one each on the shared host).
+        model.calibrate(synthetic_images(args.cal_images, seed=SEED + 1).to(dev).contiguous(), qmax)
+        scales = model.scale_dict()
+    torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         pipe.step(x)
@@ -545,7 +565,8 @@ def main():
         "vs_baseline": None,
         "dtype": "fp8_e4m3" if fp8 else "int8",
         "data": "synthetic (seeded u8 pixels normalised; seeded random-init ResNet-18 weights, "
-                f"CPU-calibrated {args.precision} scales)",
+                + (f"{args.precision} scales calibrated on the GPU over {args.cal_images} seeded images)"
+                   if args.cal_images > 0 else f"CPU-calibrated {args.precision} scales)"),
         "config": {"workload": workload,
                    "global_batch": world * B, "per_gpu_batch": B,
                    "parallelism": f"dp{world}" if world > 1 else "single",

@@ -79,6 +79,15 @@ def resnet18_state_dict(seed: int = 0x20260306) -> dict[str, np.ndarray]:
     return {k: v.float().numpy() for k, v in sd.items()}
 
 
+def site_names() -> list[str]:
+    """The 22 activation-scale sites of the int8 scheme, in
+    forward order: input, conv1, each block's conv1 / downsample / conv2, gap."""
+    out = ["input", "conv1"]
+    for name, _, _, _, ds in BLOCKS:
+        out += [f"{name}.conv1"] + ([f"{name}.downsample"] if ds else []) + [f"{name}.conv2"]
+    return out + ["gap"]
+
+
 def synthetic_images(n: int, seed: int = 0x20260306, device="cpu") -> torch.Tensor:
     """Seeded u8 pixels ~ U{0..255} normalised like tools/preprocess_to_bin.py:24-33
     ((p/255 - mean)/std) -> fp32 NCHW [n,3,224,224]."""
@@ -219,6 +228,23 @@ class ResNet18Int8:
     def scales(self, path: str) -> None:
         """Write the current activation scales (dlq_resnet18_load_scales format)."""
         self._check(self._lib.dlq_resnet18_save_scales(self.h, path.encode()), "save_scales")
+
+    def scale_dict(self) -> dict[str, float]:
+        """The current activation scales as {site: scale} (through save_scales' text)."""
+        import os
+        import tempfile
+        fd, path = tempfile.mkstemp(suffix=".txt")
+        os.close(fd)
+        try:
+            self.scales(path)
+            out = {}
+            for line in open(path):
+                parts = line.split()
+                if len(parts) == 2 and not line.startswith("#"):
+                    out[parts[0]] = float(parts[1])
+            return out
+        finally:
+            os.unlink(path)
 
     def set_timing(self, on: bool):
         self._check(self._lib.dlq_resnet18_set_timing(self.h, int(on)), "set_timing")
