@@ -176,13 +176,15 @@ class GatherPipeline:
     slot while it is in flight, and a slot is reused only after its previous
     gather has been waited on.  finish() waits for every gather in flight, so
     a timed region that ends with finish() + synchronize covers every step's
-    forward AND its all-gather.  world == 1: no exchange."""
+    forward AND its all-gather.  world == 1: no exchange (exchange=True forces
+    the collective, for a one-rank RCCL check on a one-GPU box)."""
 
-    def __init__(self, forward_into, B, world, device, depth=2):
+    def __init__(self, forward_into, B, world, device, depth=2, exchange=None):
         self.forward_into, self.world, self.depth = forward_into, world, depth
+        self.exchange = world > 1 if exchange is None else exchange
         self.logits = [torch.empty((B, 1000), dtype=torch.float32, device=device) for _ in range(depth)]
         self.out = ([torch.empty((world * B, 1000), dtype=torch.float32, device=device) for _ in range(depth)]
-                    if world > 1 else self.logits)
+                    if self.exchange else self.logits)
         self.work = [None] * depth
         self.i = 0
 
@@ -193,7 +195,7 @@ class GatherPipeline:
             self.work[k].wait()
             self.work[k] = None
         self.forward_into(x_local, self.logits[k])
-        if self.world > 1:
+        if self.exchange:
             self.work[k] = dist.all_gather_into_tensor(self.out[k], self.logits[k], async_op=True)
         return k
 

@@ -150,3 +150,55 @@ def test_dp_world8_configs3_global_batch(gpu):
     x_all = torch.cat([synthetic_images(per, seed=4000 + r) for r in range(world)]).cuda()
     ref = ResNet18Int8(sd, scales, max_batch=world * per)(x_all).cpu().numpy()
     assert np.array_equal(got.view(np.int32), ref.view(np.int32))
+
+
+def _worker_rccl(port, per, sd, scales, q):
+    """One rank over RCCL on the box's GPU: the nccl process group bound to
+    cuda:0, the engine's logits gathered by all_gather_into_tensor on device
+    tensors inside bench.GatherPipeline (the collective bench.py issues per
+    step on the 8-GPU node, here with one rank)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        import bench
+        from dlq_amd.models import ResNet18Int8, synthetic_images
+        x = synthetic_images(per, seed=77).cuda().contiguous()
+        model = ResNet18Int8(sd, scales, max_batch=per)
+        pipe = bench.GatherPipeline(lambda xx, out: model.forward(xx, out), per, 1, "cuda", exchange=True)
+        flip = torch.flip(x, dims=[0]).contiguous()
+        k1 = pipe.step(x)
+        k2 = pipe.step(flip)
+        pipe.finish()
+        p1, p2 = pipe.out[k1].cpu(), pipe.out[k2].cpu()
+        k3 = pipe.step(x)
+        pipe.finish()
+        torch.cuda.synchronize()
+        same_storage = pipe.out[k1].data_ptr() == pipe.logits[k1].data_ptr()
+        q.put((dist.get_backend(), p1.numpy(), p2.numpy(), pipe.out[k3].cpu().numpy(), (k1, k2, k3), same_storage))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_one_rank_gather_pipeline(gpu):
+    """RCCL on MI355X: communicator init and the pipeline's async
+    all_gather_into_tensor on device logits (one rank; the box has one GPU,
+    and RCCL refuses two ranks on one device).  The gathered logits are a
+    separate buffer holding the engine's logits bit for bit."""
+    from dlq_amd.models import ResNet18Int8, synthetic_images
+    from tests.helpers import model_and_scales
+    per = 64
+    sd, scales = model_and_scales()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_rccl, args=(_free_port(), per, sd, scales, q))
+    p.start()
+    backend, p1, p2, p3, slots, same = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert backend == "nccl" and slots == (0, 1, 0) and not same
+    x = synthetic_images(per, seed=77).cuda()
+    ref = ResNet18Int8(sd, scales, max_batch=per)(x).cpu().numpy()
+    assert np.array_equal(p1.view(np.int32), ref.view(np.int32))
+    assert np.array_equal(p2.view(np.int32), ref[::-1].view(np.int32))
+    assert np.array_equal(p3.view(np.int32), ref.view(np.int32))
