@@ -136,11 +136,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 
 // Work split of a launch's n_items over its blocks: logical block b =
 // xcd_remap(blockIdx.x) takes items b, b + gridDim, ... (count of them).
-// -DDLQ_X_XCDIMG instead gives b the contiguous range [first, first + count)
-// of a balanced partition, so that XCD x works on the same eighth of the
-// batch in every layer (an attempt to serve each layer's input from the L2
-// that wrote it: no gain on the wide convs, the stride-2 convs 1.5-2 us
-// slower per launch, tools/ab.py on one box).
+// (Contiguous ranges of a balanced partition instead, so that XCD x works on
+// the same eighth of the batch in every layer, were measured and removed: no
+// gain on the wide convs, the stride-2 convs 1.5-2 us slower per launch,
+// tools/ab.py on one box)
 __device__ __forceinline__ void xcd_chunk(int n_items, int& first, int& count) {
   const int Gd = gridDim.x, b = xcd_remap(blockIdx.x, Gd);
   first = b;
