@@ -24,10 +24,6 @@
 //    (same A row block) so A and B panels are reused from its L2.
 // Edge tiles and unaligned leading dimensions take byte loads with bounds
 // checks (zeros outside), interior aligned tiles vector loads.
-#include <map>
-#include <mutex>
-#include <utility>
-
 #include "device_common.h"
 
 namespace dlq {
@@ -234,10 +230,11 @@ __device__ __forceinline__ int bswz(int k) {
 // as A's (rows of 128 K bytes, chunk c at n*128 + 16*(c ^ ((n >> 1) & 7))),
 // one ds_read_b128 per B fragment instead of two ds_read_b64_tr_b8.
 //
-// One tile's K stages [sb, se) into acc (zeroed here): the whole K for the
-// data-parallel kernel, a stream-K range for gemm_s8s8s32_sk_kernel.  Loads
-// past min(K, 128 se) read zeros.  Returns with every DMA of the range
-// landed; the caller orders LDS reuse against the previous range's reads.
+// One tile's K stages [sb, se) into acc (zeroed here).  Loads past
+// min(K, 128 se) read zeros.  Returns with every DMA of the range landed.
+// (A stream-K split over [sb, se) ranges, int32 partials handed to the
+// last contributor through write-through stores, was measured bit-exact but
+// slower on every shape: DESIGN.md §6, profiles/r05_gemm_streamk.txt.)
 template <int WM, int WN, int MI, int NJ, bool BT>
 __device__ __forceinline__ void k128_tile(const int8_t* __restrict__ A, const int8_t* __restrict__ B, int M, int N,
                                           int K, int m0, int n0, int sb, int se, int8_t* lds,
@@ -373,103 +370,6 @@ __global__ __launch_bounds__(WM * WN * 64, WPS) void gemm_s8s8s32_k128_kernel(co
   k128_store<WN, MI, NJ>(C, M, N, m0, n0, acc);
 }
 
-// Stream-K (launches with fewer tiles than CUs, where whole tiles leave
-// CUs idle: 196 tiles of 256 x 256 at 256 x 50176 x 2304, 196 of 256 x 128
-// at 12544 x 512 x 4608).  The tiles' K stages, tiles * nst units in tile
-// order, are split into G equal contiguous ranges, one per workgroup
-// (G <= units, so no range is empty).  A tile covered by one range is stored
-// as usual; a tile split over ranges w_lo .. w_hi has each contributor write
-// its int32 partial (register layout) to its workspace slot (0 for its first
-// tile, 1 for its last) and count itself in cnt[tile]; the contributor that
-// counts last adds the others' partials (int32 addition: exact in any
-// order), stores the tile and resets the count for the next launch.  Nobody
-// waits for anybody, so the launch cannot deadlock whatever the residency.
-// Hand-off (cdna_hip_programming.md §6 G16, the write-through form): the
-// partials are stored sc1 (write-through, no release fence), every wave
-// drains them (vmcnt(0)) before the workgroup barrier, one lane adds to the
-// counter (relaxed, agent scope), and the last contributor reads the other
-// partials with sc1 loads only (no acquire fence).  The "last" word is
-// broadcast through the staging LDS array (no second __shared__ object).
-template <int WM, int WN, int MI, int NJ, int WPS, bool BT = false>
-__global__ __launch_bounds__(WM * WN * 64, WPS) void gemm_s8s8s32_sk_kernel(const int8_t* __restrict__ A,
-                                                                           const int8_t* __restrict__ B,
-                                                                           int32_t* __restrict__ C, int M, int N,
-                                                                           int K, int nbn, int tiles,
-                                                                           int32_t* __restrict__ ws,
-                                                                           unsigned* __restrict__ cnt) {
-  constexpr int NW = WM * WN, TM = 32 * WM * MI, TN = 32 * WN * NJ;
-  static_assert(TN == 256 || TN == 128, "B image swizzle");
-  constexpr int SA = TM * GK2, SLOT = SA + GK2 * TN;
-  constexpr int PA = TM / 8, PB = TN / 8, NP = PA + PB, PPW = NP / NW;
-  static_assert(NP % NW == 0 && PPW <= 4 * MI * NJ, "at most one piece per MFMA of a stage");
-  constexpr int TE = TM * TN;           // int32 per partial tile
-  constexpr int WE = MI * NJ * 16 * 64;  // of them per wave
-  __shared__ __attribute__((aligned(16))) int8_t lds[2 * SLOT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nst = (K + GK2 - 1) / GK2;
-  const long total = (long)tiles * nst;
-  const int G = gridDim.x, w = xcd_remap(blockIdx.x, G);
-  auto ub = [&](int x) { return (long)x * total / G; };                          // first unit of range x
-  auto owner = [&](long u) { return (int)(((u + 1) * (long)G - 1) / total); };  // the range holding unit u
-  const long u0 = ub(w), u1 = ub(w + 1);
-  const int t_first = (int)(u0 / nst);
-  const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(ws, 0, 0x7fffffff, 0x00020000);
-  constexpr int SC1 = 16;  // buffer aux: sc1 (write-through stores, L1-bypassing loads)
-  for (long u = u0; u < u1;) {
-    const int t = (int)(u / nst), sb = (int)(u - (long)t * nst);
-    const int se = (int)((long)nst < sb + (u1 - u) ? (long)nst : sb + (u1 - u));
-    const int m0 = (t / nbn) * TM, n0 = (t % nbn) * TN;
-    v16i acc[MI][NJ];
-    __syncthreads();  // every wave is past the previous range's LDS reads
-    k128_tile<WM, WN, MI, NJ, BT>(A, B, M, N, K, m0, n0, sb, se, lds, acc);
-    u += se - sb;
-    if (sb != 0 || se != nst) {
-      const int w_lo = owner((long)t * nst), w_hi = owner((long)(t + 1) * nst - 1);
-      const int mine = ((2 * w + (t == t_first ? 0 : 1)) * TE + wave * WE) * 4;  // byte offset
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            __builtin_amdgcn_raw_buffer_store_b128(
-                v4i{acc[i][j][4 * c], acc[i][j][4 * c + 1], acc[i][j][4 * c + 2], acc[i][j][4 * c + 3]}, wsr,
-                mine + (((i * NJ + j) * 4 + c) * 64 + lane) * 16, 0, SC1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial has left the CU
-      __syncthreads();
-      if (tid == 0)
-        *(volatile unsigned*)lds = __hip_atomic_fetch_add(cnt + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      const bool last = (int)*(volatile unsigned*)lds == w_hi - w_lo;
-      if (!last) continue;  // the last contributor stores the tile
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the counter
-      for (int x = w_lo; x <= w_hi; ++x) {
-        if (x == w) continue;
-        const int other = ((2 * x + (t == (int)(ub(x) / nst) ? 0 : 1)) * TE + wave * WE) * 4;
-        // two MFMA tiles' partials (8 x 16 B per lane) in flight per batch
-#pragma unroll
-        for (int ij = 0; ij < MI * NJ; ij += 2) {
-          v4i v[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            v[e] = __builtin_bit_cast(
-                v4i, __builtin_amdgcn_raw_buffer_load_b128(wsr, other + ((ij * 4 + e) * 64 + lane) * 16, 0, SC1));
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int i = (ij + e / 4) / NJ, j = (ij + e / 4) % NJ, c = e % 4;
-            acc[i][j][4 * c] += v[e][0];
-            acc[i][j][4 * c + 1] += v[e][1];
-            acc[i][j][4 * c + 2] += v[e][2];
-            acc[i][j][4 * c + 3] += v[e][3];
-          }
-        }
-      }
-      if (tid == 0) __hip_atomic_store(cnt + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    k128_store<WN, MI, NJ>(C, M, N, m0, n0, acc);
-  }
-}
-
 int num_cus_gemm() {
   static int n = 0;
   if (!n) {
@@ -501,71 +401,6 @@ int gemm_tile_for(int M, int N) {
 }
 
 namespace {
-// Stream-K workspace of one (device, stream): G x 2 partial tiles and one
-// arrival count per tile (zeroed once; each launch leaves them zero).
-// Per stream, so launches on different streams never share partial slots.
-struct SkSpace {
-  int32_t* ws = nullptr;
-  size_t ws_bytes = 0;
-  unsigned* cnt = nullptr;
-  long cnt_n = 0;
-};
-std::mutex g_sk_mu;
-std::map<std::pair<int, hipStream_t>, SkSpace> g_sk;
-
-// nullptr: no workspace (allocation failed or the stream is capturing a
-// graph and none exists yet) -- the caller takes the data-parallel kernel.
-SkSpace* sk_space(hipStream_t s, size_t ws_bytes, long tiles) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(g_sk_mu);
-  SkSpace& sp = g_sk[{dev, s}];
-  if (sp.ws_bytes >= ws_bytes && sp.cnt_n >= tiles) return &sp;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  if (hipStreamSynchronize(s) != hipSuccess) return nullptr;  // earlier launches may still use the old buffers
-  if (sp.ws) (void)hipFree(sp.ws);
-  if (sp.cnt) (void)hipFree(sp.cnt);
-  sp = SkSpace{};
-  if (hipMalloc(&sp.ws, ws_bytes) != hipSuccess) {
-    sp.ws = nullptr;
-    return nullptr;
-  }
-  if (hipMalloc(&sp.cnt, (size_t)tiles * 4) != hipSuccess || hipMemsetAsync(sp.cnt, 0, (size_t)tiles * 4, s) != hipSuccess) {
-    (void)hipFree(sp.ws);
-    if (sp.cnt) (void)hipFree(sp.cnt);
-    sp = SkSpace{};
-    return nullptr;
-  }
-  sp.ws_bytes = ws_bytes;
-  sp.cnt_n = tiles;
-  return &sp;
-}
-
-// knob "gemm_sk": 0 = stream-K when the tiles leave CUs idle (fewer tiles
-// than CUs; 256-row tiles), 1 = never, 2 = always (256-row tiles).
-bool use_sk(int cfg, long tiles) {
-  const int k = g_knob_gemm_sk.load(std::memory_order_relaxed);
-  if (cfg == 3 || k == 1) return false;
-  return k == 2 || tiles < num_cus_gemm();
-}
-
-template <int WM, int WN, int MI, int NJ, bool BT>
-hipError_t launch_sk(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, int nbn, long tiles,
-                     hipStream_t s, bool& done) {
-  constexpr int TM = 32 * WM * MI, TN = 32 * WN * NJ;
-  done = false;
-  const long units = tiles * ((K + GK2 - 1) / GK2);
-  const long G = units < num_cus_gemm() ? units : num_cus_gemm();
-  if (G < 1 || units > 0x7fffffffL / 2) return hipSuccess;
-  SkSpace* sp = sk_space(s, (size_t)G * 2 * TM * TN * 4, tiles);
-  if (!sp) return hipSuccess;
-  hipLaunchKernelGGL((gemm_s8s8s32_sk_kernel<WM, WN, MI, NJ, 1, BT>), dim3((unsigned)G), dim3(WM * WN * 64), 0, s, A, B,
-                     C, M, N, K, nbn, (int)tiles, sp->ws, sp->cnt);
-  done = true;
-  return hipGetLastError();
-}
-
 template <bool BT>
 hipError_t launch_gemm(const int8_t* A, const int8_t* B, int32_t* C, int M, int N, int K, hipStream_t s) {
   // NN: K, N multiples of 16 (B rows are 16-byte chunks of N); NT: K alone
@@ -576,12 +411,6 @@ hipError_t launch_gemm(const int8_t* A, const int8_t* B, int32_t* C, int M, int 
     const long tiles = (long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     const int nbn = (N + TN - 1) / TN;
-    if (use_sk(cfg, tiles)) {
-      bool done = false;
-      const hipError_t e = cfg == 1 ? launch_sk<2, 4, 4, 2, BT>(A, B, C, M, N, K, nbn, tiles, s, done)
-                                    : launch_sk<4, 2, 2, 2, BT>(A, B, C, M, N, K, nbn, tiles, s, done);
-      if (done || e != hipSuccess) return e;
-    }
     if (cfg == 1)
       hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<2, 4, 4, 2, 1, BT>), dim3((unsigned)tiles), dim3(512), 0, s, A, B, C,
                          M, N, K, nbn);

@@ -116,12 +116,7 @@ int dlq_pack_conv_weights_s8(const dlq_conv_desc* d, const int8_t* q_oihw, int I
  *   "head_split" (DLQ_HEAD_SPLIT) 1 = GAP and FC as two launches;
  *   "graph"      (DLQ_GRAPH)      1 = replay the forward as a hipGraph;
  *   "gemm_tile"  (DLQ_GEMM_TILE)  dlq_gemm_s8s8s32's tile, 0 = by shape,
- *                                 1 = 256 x 256, 2 = 256 x 128, 3 = 128 x 128;
- *   "gemm_sk"    (DLQ_GEMM_SK)    its stream-K split (256-row tiles), 0 = when
- *                                 the tiles are fewer than the CUs, 1 = never,
- *                                 2 = always.  Stream-K keeps a per-(device,
- *                                 stream) workspace (2 partial tiles per CU,
- *                                 <= 128 MiB), allocated at first use.
+ *                                 1 = 256 x 256, 2 = 256 x 128, 3 = 128 x 128.
  * Returns DLQ_ERR_ARG for an unknown name. */
 int dlq_set_knob(const char* name, int value);
 int dlq_get_knob(const char* name, int* value);

@@ -78,21 +78,17 @@ def test_gemm_s8s8s32_reference_layout(gpu, M, N, K):
     assert np.array_equal(Cd.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("sk", [1, 2])
 @pytest.mark.parametrize("tile", [1, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 528, 2304), (257, 400, 80), (130, 1040, 4608),
                                    (513, 144, 16), (2304, 4096, 144)])
-def test_gemm_s8s8s32_every_tile_shape(gpu, knobs, tile, sk, M, N, K):
+def test_gemm_s8s8s32_every_tile_shape(gpu, knobs, tile, M, N, K):
     """Each tile of the LDS-DMA kernel (knob gemm_tile: 1 = 256 x 256, 2 = 256 x
     128, 3 = 128 x 128; by default chosen by shape) on whole tiles, M / N / K
-    tails and K below one stage, data-parallel (knob gemm_sk 1) and stream-K
-    (gemm_sk 2, 256-row tiles: K ranges split across workgroups, partials
-    added by the last contributor; 2304 x 4096 x 144 at 256 x 128 is 288
-    tiles of 2 stages over 256 ranges, so ranges also span tile ends) --
-    bit-exact with the oracle."""
+    tails and K below one stage, and a grid of several tiles per CU in the
+    grouped raster (2304 x 4096: 9 row blocks = two full groups of 4 and a
+    group of 1) -- bit-exact with the oracle."""
     from dlq_amd.lib import lib
     knobs("gemm_tile", tile)
-    knobs("gemm_sk", sk)
     rng = np.random.default_rng(M + 3 * N + 7 * K + tile)
     A = rand_s8(rng, (M, K), lo=-128)
     B = rand_s8(rng, (K, N), lo=-128)
@@ -134,21 +130,17 @@ def test_gemm_s8s8s32_kernel_selection(gpu, M, N, K, a_off, b_off):
     assert np.array_equal(Cd.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("sk", [0, 1])
 @pytest.mark.parametrize("tile", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,N,K,a_off,b_off", [(256, 256, 128, 0, 0), (300, 521, 2304, 0, 0), (257, 400, 80, 0, 0),
                                                (130, 1040, 4608, 0, 0), (513, 7, 16, 0, 0), (100, 77, 61, 0, 0),
                                                (33, 65, 1, 0, 0), (300, 520, 128, 0, 8), (130, 264, 96, 3, 5)])
-def test_gemm_s8s8s32_nt(gpu, knobs, tile, sk, M, N, K, a_off, b_off):
+def test_gemm_s8s8s32_nt(gpu, knobs, tile, M, N, K, a_off, b_off):
     """dlq_gemm_s8s8s32_nt (B supplied as Bt[N][K]): every LDS-DMA tile on
-    whole tiles, M / N / K tails and any N (no N % 16 condition), stream-K
-    (knob gemm_sk 0: these shapes have fewer tiles than CUs) and
-    data-parallel (gemm_sk 1), and the register-staged kernel for K % 16 != 0
-    or unaligned bases (a_off / b_off), bit-exact with the oracle's NN GEMM
-    of B = Bt^T."""
+    whole tiles, M / N / K tails and any N (no N % 16 condition), and the
+    register-staged kernel for K % 16 != 0 or unaligned bases (a_off /
+    b_off), bit-exact with the oracle's NN GEMM of B = Bt^T."""
     from dlq_amd.lib import lib
     knobs("gemm_tile", tile)
-    knobs("gemm_sk", sk)
     rng = np.random.default_rng(M + 5 * N + 11 * K + tile + a_off)
     A = rand_s8(rng, (M, K), lo=-128)
     Bt = rand_s8(rng, (N, K), lo=-128)
