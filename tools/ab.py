@@ -2,7 +2,8 @@
 
 usage: python tools/ab.py [--rounds 3] [--steps 20] LIB [LIB ...]
 Each LIB is a libdlq.so path (tools/build_variant.sh); 'base' = the in-tree
-dlq_amd/libdlq.so.  Every round runs each build in its own process (the
+dlq_amd/libdlq.so; LIB@VAR=VAL runs it with VAR=VAL in the environment (a
+knob's variable, e.g. base@DLQ_STEM=2).  Every round runs each build in its own process (the
 library is chosen with DLQ_LIB_PATH), in rotating order, and prints the
 forward time and the per-family launch averages (hipEvents, rescaled to the
 timed forward as bench.py does).  With --check the first build's logits are
@@ -76,8 +77,12 @@ def main():
         order = args.libs[r % len(args.libs):] + args.libs[:r % len(args.libs)]
         for lib in order:
             env = dict(os.environ)
-            if lib != "base":
-                env["DLQ_LIB_PATH"] = os.path.abspath(lib)
+            path, _, kv = lib.partition("@")
+            if kv:
+                k, _, v = kv.partition("=")
+                env[k] = v
+            if path != "base":
+                env["DLQ_LIB_PATH"] = os.path.abspath(path)
             p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
             line = [l for l in p.stdout.splitlines() if l.startswith("ABJSON ")]
             if p.returncode != 0 or not line:
