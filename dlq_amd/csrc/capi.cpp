@@ -124,7 +124,6 @@ std::atomic<int> g_knob_l1_grid{env_int("DLQ_L1_GRID")};
 std::atomic<int> g_knob_head_split{env_int("DLQ_HEAD_SPLIT")};
 std::atomic<int> g_knob_graph{env_int("DLQ_GRAPH")};
 std::atomic<int> g_knob_gemm_tile{env_int("DLQ_GEMM_TILE")};
-std::atomic<int> g_knob_stem{env_int("DLQ_STEM")};
 // bumped by every dlq_set_knob: a forward captured as a hipGraph under other
 // knob values (head_split, l1_grid change its launches) is captured again
 std::atomic<unsigned> g_knob_gen{0};
@@ -136,7 +135,6 @@ std::atomic<int>* knob(const char* name) {
   if (!std::strcmp(name, "head_split")) return &g_knob_head_split;
   if (!std::strcmp(name, "graph")) return &g_knob_graph;
   if (!std::strcmp(name, "gemm_tile")) return &g_knob_gemm_tile;
-  if (!std::strcmp(name, "stem")) return &g_knob_stem;
   return nullptr;
 }
 }  // namespace

@@ -11,7 +11,7 @@ namespace dlq {
 
 // Host-side knobs behind dlq_set_knob (capi.cpp): initialised once from the
 // environment when the library loads, never read from it on the hot path.
-extern std::atomic<int> g_knob_l1_grid, g_knob_head_split, g_knob_graph, g_knob_gemm_tile, g_knob_stem;
+extern std::atomic<int> g_knob_l1_grid, g_knob_head_split, g_knob_graph, g_knob_gemm_tile;
 extern std::atomic<unsigned> g_knob_gen;
 
 

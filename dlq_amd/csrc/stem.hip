@@ -733,307 +733,6 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
   }
 }
 
-// stem3_kernel: stem2_kernel's work with the roles split across the waves
-// of one workgroup (one per CU, 8 waves = 2 per SIMD): waves 0-3 (column
-// quarter q = wave) hold the weights and run only the conv MFMAs and the
-// int32 pooling; waves 4-7 (quarter q = wave - 4) load and quantise the input
-// into the conv-row ring and run the previous step's epilogue (requant,
-// staging transpose, NHWC store) from the pooled int32 the MFMA wave of
-// their quarter left in LDS.  Each SIMD then holds one MFMA wave and one
-// VALU wave whose work overlaps, where stem2's two full-step waves per SIMD
-// contend for the same issue slots in the same phase.  Same ring, band
-// logic, pooling and numerics as stem2_kernel (bit-identical).
-constexpr int S3W = 8;
-constexpr int HO3 = 4 * 64 * 16;  // pooled hand-off per quarter: [4 quads][64 lanes][16 B]
-constexpr int OFF_HO3 = OFF_STAGE2 + S2W * STG2;
-constexpr int LDS_STEM3 = OFF_HO3 + 2 * 4 * HO3;
-static_assert(LDS_STEM3 <= 160 * 1024, "one workgroup per CU");
-
-__global__ __launch_bounds__(S3W * 64, 1) void stem3_kernel(StemArgs a) {
-  __shared__ __attribute__((aligned(16))) int8_t lds[LDS_STEM3];
-  const unsigned lds32 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) int8_t*)lds;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = wave & 3;
-  const int lr = lane & 31, lh = lane >> 5;
-  const int nitems = a.N * a.nb;
-  for (int i = tid; i < CR_SLOTS * CR_ROW / 16; i += S3W * 64) *(v4i*)(lds + OFF_CR + i * 16) = v4i{0, 0, 0, 0};
-  __syncthreads();
-  int item0, n_my;
-  xcd_chunk(nitems, item0, n_my);
-  int8_t* ho = lds + OFF_HO3 + q * HO3 + lane * 16;  // + buf * 4 * HO3 + quad * 1024
-
-  if (wave < 4) {
-    // ---- MFMA waves ----
-    v4i wr[2][6];
-#pragma unroll
-    for (int ot = 0; ot < 2; ++ot)
-#pragma unroll
-      for (int t = 0; t < 6; ++t) wr[ot][t] = *(const v4i*)(a.w + (ot * 32 + lr) * SK + t * 32 + lh * 16);
-    const int pi = ((lr >> 3) << 2) + (lr & 3) + 16 * ((lr >> 2) & 1);
-    const int ox = 28 * q - 1 + pi;
-    const unsigned a_col = lds32 + OFF_CR + (unsigned)(ox + 2 + lh) * 16;
-    // conv rows oy, oy + 1 into c; mid(k) runs after k-step k's MFMAs are
-    // issued (the previous step's pooling, spread beside the matrix pipe)
-    auto conv_rows2 = [&](int oy, v16i (&c)[2][2], auto&& mid) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) c[i][0] = c[i][1] = v16i{0};
-      const unsigned ra0 = a_col + (oy & (CR_SLOTS - 1)) * CR_ROW, ra1 = a_col + ((oy + 1) & (CR_SLOTS - 1)) * CR_ROW;
-      // A fragments four k-steps ahead (one MFMA wave per SIMD: nothing else
-      // hides their latency; a fifth and sixth pair would not fit beside
-      // the two accumulator sets), consumed in issue order (LDS returns in
-      // order, so the hand-off writes of mid() only make a wait stricter)
-      v4i fa0[4], fa1[4];
-#define STEM3_RD(t)                                                                                              \
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa0[(t) & 3]) : "v"(ra0), "n"(((t) >> 1) * CR_PLANE + ((t) & 1) * 32) \
-               : "memory");                                                                                      \
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa1[(t) & 3]) : "v"(ra1), "n"(((t) >> 1) * CR_PLANE + ((t) & 1) * 32) \
-               : "memory")
-#define STEM3_WAIT(t, n) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(fa0[(t) & 3]), "+v"(fa1[(t) & 3]) : "n"(n) : "memory")
-#define STEM3_K(t)                                                                          \
-  c[0][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0[(t) & 3], wr[0][t], c[0][0], 0, 0, 0); \
-  c[0][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0[(t) & 3], wr[1][t], c[0][1], 0, 0, 0); \
-  c[1][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1[(t) & 3], wr[0][t], c[1][0], 0, 0, 0); \
-  c[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1[(t) & 3], wr[1][t], c[1][1], 0, 0, 0)
-      STEM3_RD(0);
-      STEM3_RD(1);
-      STEM3_RD(2);
-      STEM3_RD(3);
-      STEM3_WAIT(0, 6);
-      STEM3_K(0);
-      STEM3_RD(4);
-      mid(std::integral_constant<int, 0>{});
-      STEM3_WAIT(1, 6);
-      STEM3_K(1);
-      STEM3_RD(5);
-      mid(std::integral_constant<int, 1>{});
-      STEM3_WAIT(2, 6);
-      STEM3_K(2);
-      mid(std::integral_constant<int, 2>{});
-      STEM3_WAIT(3, 4);
-      STEM3_K(3);
-      mid(std::integral_constant<int, 3>{});
-      STEM3_WAIT(4, 2);
-      STEM3_K(4);
-      mid(std::integral_constant<int, 4>{});
-      STEM3_WAIT(5, 0);
-      STEM3_K(5);
-      mid(std::integral_constant<int, 5>{});
-#undef STEM3_RD
-#undef STEM3_WAIT
-#undef STEM3_K
-    };
-    auto hpool = [&](const v16i& c, int (&H)[8]) {
-      unsigned x0 = (unsigned)c[0], c16 = x0;
-      swap32(x0, c16);
-      const int c0v = (q == 0 && lh == 0) ? kIntMin : c[0];
-      H[0] = max3i(c0v, c[1], c[2]);
-#pragma unroll
-      for (int m = 1; m < 7; ++m) H[m] = max3i(c[2 * m], c[2 * m + 1], c[2 * m + 2]);
-      H[7] = max3i(c[14], c[15], (int)c16);
-    };
-    for (int li = 0; li < n_my; ++li) {
-      const int item = xcd_item(item0, li);
-      const int n = item / a.nb, band = item - n * a.nb;
-      const int py0 = band * a.R, py1 = min(56, py0 + a.R);
-      if (py0 >= py1) continue;
-      __builtin_amdgcn_s_barrier();  // the converters' prologue quads are in the ring
-      auto none = [](auto) {};
-      int Hp[2][8];
-      if (py0 == 0) {
-#pragma unroll
-        for (int ot = 0; ot < 2; ++ot)
-#pragma unroll
-          for (int m = 0; m < 8; ++m) Hp[ot][m] = kIntMin;
-      } else {
-        v16i c[2][2];
-        conv_rows2(2 * py0 - 1, c, none);
-        hpool(c[0][0], Hp[0]);
-        hpool(c[0][1], Hp[1]);
-      }
-      // step t's MFMAs run beside the pooling of step t - 1 (its pooled
-      // row goes to hand-off buffer (t - 1) & 1; the converters requantise
-      // it one step later)
-      int He[8], Ho[8], v[8];
-      auto pool_into = [&](const v16i (&pc)[2][2], int tp, auto k) {
-        constexpr int K = decltype(k)::value;
-        constexpr int ot = K < 3 ? 0 : 1;
-        if constexpr (K == 0 || K == 3) {
-          hpool(pc[0][ot], He);
-          hpool(pc[1][ot], Ho);
-        } else if constexpr (K == 1 || K == 4) {
-#pragma unroll
-          for (int m = 0; m < 8; ++m) {
-            v[m] = max3i(Hp[ot][m], He[m], Ho[m]);
-            Hp[ot][m] = Ho[m];
-          }
-        } else {
-          int8_t* hb = ho + (tp & 1) * 4 * HO3 + ot * 2048;
-          *(v4i*)hb = v4i{v[0], v[1], v[2], v[3]};
-          *(v4i*)(hb + 1024) = v4i{v[4], v[5], v[6], v[7]};
-        }
-      };
-      const int T = py1 - py0;
-      v16i cA[2][2], cB[2][2];
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_s_barrier();
-      conv_rows2(2 * py0, cA, none);
-      int t = 1;
-      for (; t + 2 <= T; t += 2) {
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_s_barrier();
-        conv_rows2(2 * (py0 + t), cB, [&](auto k) { pool_into(cA, t - 1, k); });
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_s_barrier();
-        conv_rows2(2 * (py0 + t + 1), cA, [&](auto k) { pool_into(cB, t, k); });
-      }
-      if (t < T) {
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_s_barrier();
-        conv_rows2(2 * (py0 + t), cB, [&](auto k) { pool_into(cA, t - 1, k); });
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_s_barrier();  // "step T": the last step's pooling
-        pool_into(cB, T - 1, std::integral_constant<int, 0>{});
-        pool_into(cB, T - 1, std::integral_constant<int, 1>{});
-        pool_into(cB, T - 1, std::integral_constant<int, 2>{});
-        pool_into(cB, T - 1, std::integral_constant<int, 3>{});
-        pool_into(cB, T - 1, std::integral_constant<int, 4>{});
-        pool_into(cB, T - 1, std::integral_constant<int, 5>{});
-      } else {
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_s_barrier();  // "step T": the last step's pooling
-        pool_into(cA, T - 1, std::integral_constant<int, 0>{});
-        pool_into(cA, T - 1, std::integral_constant<int, 1>{});
-        pool_into(cA, T - 1, std::integral_constant<int, 2>{});
-        pool_into(cA, T - 1, std::integral_constant<int, 3>{});
-        pool_into(cA, T - 1, std::integral_constant<int, 4>{});
-        pool_into(cA, T - 1, std::integral_constant<int, 5>{});
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_s_barrier();  // the last pooled row is in LDS
-      __syncthreads();               // item end: the converters are done with the ring and the hand-off
-    }
-  } else {
-    // ---- converter / epilogue waves ----
-    const float al[2] = {a.alpha[lr], a.alpha[32 + lr]}, be[2] = {a.beta[lr], a.beta[32 + lr]};
-    const int cv_p = lh, cv_u = lr + 32 * q;
-    const bool col_ok = (unsigned)(cv_u - 4) < 112u;
-    int8_t* stg = lds + OFF_STAGE2 + q * STG2;
-    const int tg = lane >> 4, ti = lane & 15;
-    const int R1 = 16 * tg + 8 * (tg & 1) + (ti >> 1), R2 = 16 * tg + 8 * (1 - (tg & 1)) + (ti >> 1);
-    const int8_t* tr1 = stg + R1 * 16 + 8 * ((ti & 1) ^ ((R1 >> 3) & 1));
-    const int8_t* tr2 = stg + R2 * 16 + 8 * ((ti & 1) ^ ((R2 >> 3) & 1));
-    for (int li = 0; li < n_my; ++li) {
-      const int item = xcd_item(item0, li);
-      const int n = item / a.nb, band = item - n * a.nb;
-      const int py0 = band * a.R, py1 = min(56, py0 + a.R);
-      if (py0 >= py1) continue;
-      const int iy0 = 4 * py0 - 5;
-      const float* img = a.x + (size_t)n * 3 * 224 * 224;
-      using F2 = float __attribute__((ext_vector_type(2)));
-      F2 raw[PD + 1][2][3];
-      __amdgpu_buffer_rsrc_t rs[3];
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-        rs[c] = __builtin_amdgcn_make_buffer_rsrc((void*)(img + (size_t)c * 224 * 224), 0, 224 * 224 * 4, 0x00020000);
-      auto load_quad = [&](int k, F2 (&r)[2][3]) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int iy = iy0 + 4 * k + 2 * cv_p + h, sc = cv_u - 4;
-          const int off = ((unsigned)iy < 224u && col_ok) ? (iy * 224 + 2 * sc) * 4 : 0x40000000;
-#pragma unroll
-          for (int c = 0; c < 3; ++c)
-            r[h][c] = __builtin_bit_cast(F2, __builtin_amdgcn_raw_buffer_load_b64(rs[c], off, 0, 0));
-        }
-      };
-      const int ob0 = ((iy0 - 3) >> 1) + cv_p;
-      int sa[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sa[j] = OFF_CR + ((ob0 + j) & (CR_SLOTS - 1)) * CR_ROW + cv_u * 16;
-      auto convert_quad = [&](const F2 (&r)[2][3], auto jc) {
-        constexpr int J = decltype(jc)::value;
-        unsigned v[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          unsigned u[4];
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int d = 0; d < 2; ++d)
-              u[2 * h + d] = __float_as_uint(__builtin_amdgcn_fmed3f(r[h][c][d] * a.inv_s, -127.f, 127.f) + 12582912.0f);
-          v[c] = __builtin_amdgcn_perm(u[1], u[0], 0x0c0c0400u) | __builtin_amdgcn_perm(u[3], u[2], 0x04000c0cu);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int c = 0; c < 3; ++c) *(unsigned*)(lds + sa[(J + e) & 7] + (12 - 4 * e + c * CR_PLANE)) = v[c];
-      };
-      // pooled row p from hand-off buffer b: requant, staging transpose, NHWC store
-      auto epilogue = [&](int p, int b) {
-        const int8_t* hb = ho + b * 4 * HO3;
-        v4i h[4];
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4) h[c4] = *(const v4i*)(hb + c4 * 1024);
-#pragma unroll
-        for (int ot = 0; ot < 2; ++ot) {
-          unsigned w[2] = {0u, 0u};
-#pragma unroll
-          for (int m = 0; m < 8; ++m) {
-            const float y = __builtin_fmaf((float)h[2 * ot + (m >> 2)][m & 3], al[ot], be[ot]);
-            w[m >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(y, 127.f), m & 3, w[m >> 2]);
-          }
-          const int row = ot * 32 + lr;
-          *(v2i*)(stg + row * 16 + 8 * (lh ^ ((row >> 3) & 1))) = v2i{(int)w[0], (int)w[1]};
-        }
-        asm volatile("" ::: "memory");  // the staging writes stay above the transposed reads (in-order LDS per wave)
-        const v2i r1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)tr1);
-        const v2i r2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)tr2);
-        const v4i o = (tg & 1) ? v4i{r2[0], r2[1], r1[0], r1[1]} : v4i{r1[0], r1[1], r2[0], r2[1]};
-        if (ti < 14) *(v4i*)(a.y + (((size_t)n * 56 + p) * 56 + 14 * q + ti) * 64 + 16 * tg) = o;
-      };
-#pragma unroll
-      for (int k = 0; k <= PD; ++k) load_quad(k, raw[k]);
-      convert_quad(raw[0], std::integral_constant<int, 0>{});
-      load_quad(PD + 1, raw[0]);
-      convert_quad(raw[1], std::integral_constant<int, 2>{});
-      load_quad(PD + 2, raw[1]);
-      convert_quad(raw[2], std::integral_constant<int, 4>{});
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_s_barrier();
-      auto step = [&](int t, auto setc) {
-        constexpr int S = decltype(setc)::value;
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_s_barrier();
-        convert_quad(raw[(S + 3) % (PD + 1)], std::integral_constant<int, (2 * S + 6) & 7>{});
-        load_quad(t + 3 + PD, raw[(S + 2) % (PD + 1)]);
-        if (t > 1) epilogue(py0 + t - 2, t & 1);
-      };
-      const int nsteps = py1 - py0;
-      static_assert(PD == 3, "the step loop below is unrolled by 4");
-      using I0 = std::integral_constant<int, 0>;
-      using I1 = std::integral_constant<int, 1>;
-      using I2 = std::integral_constant<int, 2>;
-      using I3 = std::integral_constant<int, 3>;
-      int t = 0;
-      for (; t + 4 <= nsteps; t += 4) {
-        step(t, I0{});
-        step(t + 1, I1{});
-        step(t + 2, I2{});
-        step(t + 3, I3{});
-      }
-      if (t < nsteps) step(t, I0{});
-      if (t + 1 < nsteps) step(t + 1, I1{});
-      if (t + 2 < nsteps) step(t + 2, I2{});
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_s_barrier();  // "step T"
-      if (nsteps > 1) epilogue(py1 - 2, nsteps & 1);
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_s_barrier();  // the last pooled row is in LDS
-      epilogue(py1 - 1, (nsteps - 1) & 1);
-      wait_vm0();
-      __syncthreads();
-    }
-  }
-}
-
 int num_cus_stem() {
   static int n = 0;
   if (!n) {
@@ -1092,20 +791,8 @@ hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float
   const int items = N * nb, grid = items < 2 * ncu ? items : 2 * ncu;
   if (f8)
     hipLaunchKernelGGL(stem_fused_kernel<true>, dim3(grid), dim3(SNW * 64), 0, s, a);
-  else if (g_knob_stem.load(std::memory_order_relaxed) == 2)
+  else
     hipLaunchKernelGGL(stem2_kernel, dim3(grid), dim3(S2W * 64), 0, s, a);
-  else {
-    // one workgroup per CU: one band per CU where the batch allows (a band's
-    // prologue -- 4 input quads loaded, 3 converted -- is not hidden behind
-    // another workgroup's steps as in stem2's two per CU)
-    int nb3 = (ncu + N - 1) / N;
-    nb3 = nb3 < 1 ? 1 : (nb3 > 14 ? 14 : nb3);
-    const int R3 = (56 + nb3 - 1) / nb3;
-    nb3 = (56 + R3 - 1) / R3;
-    const StemArgs a3{x, w, alpha, beta, y, inv_s, N, nb3, R3};
-    const int items3 = N * nb3;
-    hipLaunchKernelGGL(stem3_kernel, dim3(items3 < ncu ? items3 : ncu), dim3(S3W * 64), 0, s, a3);
-  }
   return hipGetLastError();
 }
 
