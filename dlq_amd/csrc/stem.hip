@@ -587,6 +587,24 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
     int sa[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) sa[j] = OFF_CR + ((ob0 + j) & (CR_SLOTS - 1)) * CR_ROW + cv_u * 16;
+    // scatter addresses with the conv-row order rotated per 16-lane group:
+    // write i of group g goes to conv row e = (i + g) & 3, so the four
+    // groups' 4-byte writes land at chunk offsets 12 - 4e that differ mod 16
+    // bytes -- 64 distinct banks per instruction, where the same e for every
+    // lane put all four groups on the same 16 banks
+    const int lg = (tid >> 4) & 3;
+    int ra[4][4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = (i + lg) & 3;
+        int v = sa[(2 * jj) & 7];
+        v = e == 1 ? sa[(2 * jj + 1) & 7] : v;
+        v = e == 2 ? sa[(2 * jj + 2) & 7] : v;
+        v = e == 3 ? sa[(2 * jj + 3) & 7] : v;
+        ra[jj][i] = v + 12 - 4 * e;
+      }
     auto convert_quad = [&](const F2 (&r)[2][3], auto jc) {  // jc = (2k) & 7
       constexpr int J = decltype(jc)::value;
       unsigned v[3];
@@ -601,9 +619,9 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
         v[c] = __builtin_amdgcn_perm(u[1], u[0], 0x0c0c0400u) | __builtin_amdgcn_perm(u[3], u[2], 0x04000c0cu);
       }
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) *(unsigned*)(lds + sa[(J + e) & 7] + (12 - 4 * e + c * CR_PLANE)) = v[c];
+        for (int c = 0; c < 3; ++c) *(unsigned*)(lds + ra[J >> 1][i] + c * CR_PLANE) = v[c];
     };
     // conv rows oy, oy + 1 x both channel tiles: four chains per k-step on the
     // A fragments of the two rows (read once) and the resident weights
