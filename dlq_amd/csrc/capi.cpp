@@ -124,6 +124,7 @@ std::atomic<int> g_knob_l1_grid{env_int("DLQ_L1_GRID")};
 std::atomic<int> g_knob_head_split{env_int("DLQ_HEAD_SPLIT")};
 std::atomic<int> g_knob_graph{env_int("DLQ_GRAPH")};
 std::atomic<int> g_knob_gemm_tile{env_int("DLQ_GEMM_TILE")};
+std::atomic<int> g_knob_ds_split{env_int("DLQ_DS_SPLIT")};
 // bumped by every dlq_set_knob: a forward captured as a hipGraph under other
 // knob values (head_split, l1_grid change its launches) is captured again
 std::atomic<unsigned> g_knob_gen{0};
@@ -135,6 +136,7 @@ std::atomic<int>* knob(const char* name) {
   if (!std::strcmp(name, "head_split")) return &g_knob_head_split;
   if (!std::strcmp(name, "graph")) return &g_knob_graph;
   if (!std::strcmp(name, "gemm_tile")) return &g_knob_gemm_tile;
+  if (!std::strcmp(name, "ds_split")) return &g_knob_ds_split;
   return nullptr;
 }
 }  // namespace
@@ -309,6 +311,26 @@ int dlq_conv2d_s2_ds_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8
   if (a.P == 0) return DLQ_OK;
   hipError_t e = launch_conv3x3s2i(a, w_ds, alpha_ds, beta_ds, y_ds, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d_s2_ds launch: ") + hipGetErrorString(e));
+}
+
+int dlq_conv2d_dsres_nhwc_s8(const dlq_conv_desc* d, const int8_t* h, const int8_t* w_packed, const float* alpha,
+                             const float* beta, const int8_t* x_blk, const int8_t* w_ds, const float* alpha_ds,
+                             const float* beta_ds, float res_scale, int8_t* y, void* stream) {
+  if (!d || !conv3x3w_shape(DLQ_DESC_GEOM(d)))
+    return fail(DLQ_ERR_ARG, "conv2d_dsres: needs a 3x3/s1/p1 C->C conv at 28x28x128, 14x14x256 or 7x7x512");
+  if (!x_blk || !w_ds || !alpha_ds || !beta_ds) return fail(DLQ_ERR_ARG, "conv2d_dsres: null pointer");
+  ConvArgs a;
+  bool wide = false;
+  int rc = conv_args(d, h, w_packed, alpha, beta, nullptr, res_scale, 1, DLQ_OUT_S8, y, a, wide);
+  if (rc) return rc;
+  if (a.P == 0) return DLQ_OK;
+  a.ds_x = x_blk;
+  a.ds_w = w_ds;
+  a.ds_alpha = alpha_ds;
+  a.ds_beta = beta_ds;
+  a.ds_C = d->C / 2;
+  hipError_t e = launch_conv3x3i_dsr(a, (hipStream_t)stream);
+  return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d_dsres launch: ") + hipGetErrorString(e));
 }
 
 int dlq_block_l1_nhwc_s8(const int8_t* x, int N, const int8_t* w1, const float* alpha1, const float* beta1,

@@ -138,6 +138,38 @@ __device__ __forceinline__ void wave_tiles(int wave, int& mt, int& f0, int& nf) 
 // The kernel's LDS constants (zero region, alpha/beta): written after stage
 // 0's DMA is issued so their global-load latency overlaps it; stage 0's
 // barrier publishes them.
+// s_waitcnt vmcnt(N) tied to the fragments it waits for (untracked loads,
+// gload16_untracked): their later uses are ordered after the wait and no
+// copy of an in-flight register can be made before it.
+template <int N, int K>
+__device__ __forceinline__ void wait_vm_tie_frags(v4i (&x)[K]) {
+  static_assert(K == 1 || K == 2 || K == 4 || K == 8, "fragment counts of the DSR downsample");
+  if constexpr (K == 1)
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(x[0]) : "n"(N) : "memory");
+  else if constexpr (K == 2)
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(x[0]), "+v"(x[1]) : "n"(N) : "memory");
+  else if constexpr (K == 4)
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]) : "n"(N) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7])
+                 : "n"(N)
+                 : "memory");
+}
+// register ties without a wait (after a runtime-count wait_vm)
+template <int K>
+__device__ __forceinline__ void tie_frags(v4i (&x)[K]) {
+#pragma unroll
+  for (int i = 0; i < K; ++i) asm volatile("" : "+v"(x[i]));
+}
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for_i(F& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_i<I + 1, N>(f);
+  }
+}
+
 template <int W, int C, int OUT, int SPS>
 __device__ __forceinline__ void conv3x3i_init(const ConvArgs& a, int8_t* lds) {
   using G = IGeo<W, SPS>;
@@ -254,8 +286,20 @@ struct WideStream {
 
 // RELU (int8, OUT == 0): the output clamp is [0, 127] and the requantisation
 // takes the v_cvt_pk_u8_f32 form (device_common.h quant4_relu).
-template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false, bool RELU = false>
+// DSR (int8, RES, RELU): a downsampling block's conv2, whose residual is the
+// block's 1x1/s2 downsample (infer_e2e.cu:187-199) computed here instead of
+// read: per tile KD = C/64 v_mfma_i32_32x32x32_i8 on A fragments of the
+// downsample weights (the wave's 32 channels, loaded once per item) and B
+// fragments of the block input at (2 oh, 2 ow) (16 bytes per lane and k-step,
+// loaded one tile ahead), requantised exactly as the downsample's own epilogue
+// (device_common.h epi4_dsr_relu).  int32 sums are order-free, so the
+// residual is bit-identical to the fused stride-2 kernel's downsample output;
+// that kernel then runs conv1 alone.
+template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false, bool RELU = false, bool DSR = false>
 __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int wave, int mt, int f0) {
+  static_assert(!DSR || (OUT == 0 && RES && RELU && !F8), "the downsample residual is an int8 ReLU epilogue");
+  constexpr bool RESL = RES;  // the residual is loaded (DSR: from y, where the item's downsample was stored)
+  constexpr int KD = C / 64;          // DSR: downsample k-steps (the block input has C/2 channels)
   constexpr int SPS = sps_of<W, F8>();
   using G = IGeo<W, SPS>;
   constexpr int NS = C / ISC / SPS;  // stages (SPS 32-channel slices each)
@@ -305,12 +349,113 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   Acc acc[NF];
   v4i rq[NF];
   int cur_ot = 0, cur_p0 = 0;
+  // DSR: the item's downsample, computed before its first stage's MFMAs
+  // (ds_issue + ds_compute): A fragments of the downsample weights (this
+  // wave's 32 channels; k-step kk = block-input channels 32 kk + 16 lh ..),
+  // its alpha / beta, and B fragments of each tile's pixels at (2 oh, 2 ow)
+  // of the block input through a ring of RB tiles; the int8 results stay in
+  // rds[f] (MFMA layout: byte e of rds[f][g] = channel 8 g + 4 lh + e) until
+  // the item's epilogue adds them as the residual.
+  constexpr int KDA = DSR ? KD : 1;
+  constexpr int RB = !DSR ? 1 : KD <= 2 ? NF : KD == 4 ? 3 : 2;
+  v4i ads[KDA], dab[DSR ? 8 : 1], bq[RB][KDA];
+  int ds_ot = 0, ds_p0 = 0;
+  auto ds_bload = [&](int f, v4i(&b)[KDA]) {
+    const int lp = (f0 + f) * 32 + lr, p = ds_p0 + lp;
+    const int pp = lp < IL && p < a.P ? p : 0;
+    const int n = pp / (W * W), r = pp - n * (W * W), oh = r / W, ow = r - oh * W;
+    const int8_t* src = a.ds_x + (size_t)((n * 2 * W + 2 * oh) * 2 * W + 2 * ow) * (C / 2) + lh * 16;
+#pragma unroll
+    for (int kk = 0; kk < KDA; ++kk) b[kk] = gload16_untracked(src + kk * 32);
+  };
+  auto ds_issue = [&](int li) {  // the item's loads: A fragments, alpha / beta, the first RB tiles
+    if constexpr (!DSR) return;
+    item_of(li, ds_ot, ds_p0);
+    const int o = ds_ot * G::OT + mt * 32 + lr;
+#pragma unroll
+    for (int kk = 0; kk < KDA; ++kk)
+      ads[kk] = gload16_untracked(a.ds_w + ((size_t)((o >> 7) * KD + kk) * 128 + (o & 127)) * 48 + lh * 16);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int oc = ds_ot * G::OT + mt * 32 + 8 * g + 4 * lh;
+      dab[2 * g] = gload16_untracked(a.ds_alpha + oc);
+      dab[2 * g + 1] = gload16_untracked(a.ds_beta + oc);
+    }
+#pragma unroll
+    for (int f = 0; f < RB; ++f) ds_bload(f, bq[f]);
+  };
+  // FIRST: the first item's stage-0 LDS-DMA was issued between ds_issue and
+  // ds_compute, so it is younger than the first RB tiles' loads; the waits
+  // count it as the fewest unmasked pieces any wave issues (a lower bound on
+  // what vmcnt counts: safe whether masked pieces count or not)
+  auto ds_compute = [&](auto first_c) {
+    if constexpr (DSR) {
+      constexpr int NDMA = decltype(first_c)::value ? G::PPS / NLD + G::WPS / NLD : 0;
+      // tile f's downsample requantised as its own epilogue would (conv3x3s2i
+      // DS: signed clamp) and stored, in the store layout, where the item's
+      // output goes: the epilogue reads it back as the residual (this wave's
+      // own bytes, an L2 hit) and overwrites it
+      auto requant = [&](const v16i& ac, int f) {
+        unsigned q[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float al4[4] = {__int_as_float(dab[2 * g][0]), __int_as_float(dab[2 * g][1]),
+                                __int_as_float(dab[2 * g][2]), __int_as_float(dab[2 * g][3])};
+          const float be4[4] = {__int_as_float(dab[2 * g + 1][0]), __int_as_float(dab[2 * g + 1][1]),
+                                __int_as_float(dab[2 * g + 1][2]), __int_as_float(dab[2 * g + 1][3])};
+          const int a4[4] = {ac[4 * g], ac[4 * g + 1], ac[4 * g + 2], ac[4 * g + 3]};
+          q[g] = epi4(a4, al4, be4, -127.f);
+        }
+        swap32(q[0], q[2]);
+        swap32(q[1], q[3]);
+        const int lp = (f0 + f) * 32 + lr, p = ds_p0 + lp;
+        const bool keep = lp < IL && p < a.P;
+        v4i* dst = keep ? (v4i*)((int8_t*)a.y + (size_t)p * a.OC + ds_ot * G::OT + mt * 32 + lh * 16)
+                        : (v4i*)(g_trash_i + lane * 16);
+        *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
+      };
+      v16i prev = v16i{0};
+      auto tile = [&](auto fc) {
+        constexpr int f = decltype(fc)::value;
+        // younger than tile f's loads: the later tiles issued so far (and the DMA)
+        constexpr int CNT = ((f + RB - 1 < NF - 1 ? f + RB - 1 : NF - 1) - f) * KDA + (f < RB ? NDMA : 0);
+        v4i(&b)[KDA] = bq[f % RB];
+        wait_vm_tie_frags<CNT>(b);
+        if constexpr (f == 0) {
+          tie_frags(ads);
+          tie_frags(dab);
+        }
+        v16i accd = v16i{0};
+#pragma unroll
+        for (int kk = 0; kk < KDA; ++kk) accd = __builtin_amdgcn_mfma_i32_32x32x32_i8(ads[kk], b[kk], accd, 0, 0, 0);
+        if constexpr (f > 0) requant(prev, f - 1);
+        if constexpr (f + RB < NF) ds_bload(f + RB, b);
+        prev = accd;
+      };
+      static_for_i<0, NF>(tile);
+      requant(prev, NF - 1);
+    }
+  };
 
   ISTAMP(0);
+  // DSR: the first item's downsample loads go out ahead of stage 0's DMA, and
+  // its MFMAs and requantisation run while that DMA lands (the launch's cold
+  // prologue)
+  if constexpr (DSR) ds_issue(0);
   if (loader) {
     prep_for(0);
 #pragma unroll
     for (int k = 0; k < DPW; ++k) issue_piece(0, k);
+  }
+  if constexpr (DSR) {
+    ds_compute(std::true_type{});
+    // the workgroup's later items (two per CU in the 28x28 launch): stored
+    // the same way now, not between items -- a downsample phase inside the
+    // stage loop made the compiler spill the k-loop's registers
+    for (int li = 1; li < st.nst / NS; ++li) {
+      ds_issue(li);
+      ds_compute(std::false_type{});
+    }
   }
   if (DLQ_ABL(a, 256)) {  // probe builds: stage 0 landed from a cold L2, then the same pieces again (L2-hot)
     wait_vm_const<0>();
@@ -394,7 +539,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
           const int i = pr * NF + f;
           acc[f] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa2[pr & 1], fbr[i % D], acc[f], 0, 0, 0, 0, 0, 0);
           if (i + D < NM) fbr[i % D] = ld_b2(i + D);
-          if constexpr (OUT == 0 && RES) {
+          if constexpr (OUT == 0 && RESL) {
             if (pr == NPAIR - 1 && j == NS - 1) {
               const int p = cur_p0 + (f0 + f) * 32 + lr;
               const bool keep = (f0 + f) * 32 + lr < IL && p < a.P;
@@ -415,7 +560,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       const int p = cur_p0 + (f0 + f) * 32 + lr;
       const bool keep = (f0 + f) * 32 + lr < IL && p < a.P;
       const size_t off = keep ? (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16 : 0;
-      rq[f] = gload16_untracked(a.res + off);
+      rq[f] = gload16_untracked((DSR ? (const int8_t*)a.y : a.res) + off);
     };
     if constexpr (PF2) {
     // B fragments two k-steps ahead: fb[ks & 1][f] holds k-step ks of tile f
@@ -444,7 +589,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
         acc[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu], fb[bu][f], acc[f], 0, 0, 0);
         if (f == NF - 1 && ks + 2 < KSN) fa[bu] = a_at(ks + 2);
         if (ks + 2 < KSN && !DLQ_ABL(a, 8)) ld_b(ks + 2, f);  // probe builds: dbg 8 re-uses k-steps 0/1's B
-        if constexpr (OUT == 0 && RES) {
+        if constexpr (OUT == 0 && RESL) {
           if (ks == KSN - 1 && j == NS - 1) res_load(f);
         }
       }
@@ -489,7 +634,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       for (int f = 0; f < NF; ++f) {
         acc[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu], fb[f], acc[f], 0, 0, 0);
         if (ks + 1 < KSN && !DLQ_ABL(a, 8)) ld_b(ks + 1, f);  // probe builds: dbg 8 re-uses k-step 0's B
-        if constexpr (OUT == 0 && RES) {
+        if constexpr (OUT == 0 && RESL) {
           // into the registers this tile's last B fragment just freed
           if (ks == KSN - 1 && j == NS - 1) res_load(f);
         }
@@ -609,7 +754,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   ISTAMP(63);
 }
 
-template <int W, int C, int OUT, bool RES, bool F8 = false, bool RELU = false>
+template <int W, int C, int OUT, bool RES, bool F8 = false, bool RELU = false, bool DSR = false>
 __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   using G = IGeo<W, sps_of<W, F8>()>;
   constexpr int OFF_AB = G::OFF_AB;
@@ -624,14 +769,14 @@ __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   // for every wave, WideStream): two bodies per kernel
   if constexpr (G::MT == 4) {
     if (wave < 4)
-      conv3x3i_body<W, C, OUT, RES, 7, INW, F8, RELU>(a, lds, wave, mt, f0);
+      conv3x3i_body<W, C, OUT, RES, 7, INW, F8, RELU, DSR>(a, lds, wave, mt, f0);
     else
-      conv3x3i_body<W, C, OUT, RES, 6, INW, F8, RELU>(a, lds, wave, mt, f0);
+      conv3x3i_body<W, C, OUT, RES, 6, INW, F8, RELU, DSR>(a, lds, wave, mt, f0);
   } else {
     if (wave < 2)
-      conv3x3i_body<W, C, OUT, RES, 4, INW, F8, RELU>(a, lds, wave, mt, f0);
+      conv3x3i_body<W, C, OUT, RES, 4, INW, F8, RELU, DSR>(a, lds, wave, mt, f0);
     else
-      conv3x3i_body<W, C, OUT, RES, 3, INW, F8, RELU>(a, lds, wave, mt, f0);
+      conv3x3i_body<W, C, OUT, RES, 3, INW, F8, RELU, DSR>(a, lds, wave, mt, f0);
   }
   (void)nf;
 }
@@ -665,7 +810,32 @@ hipError_t launch_ci(const ConvArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int W, int C>
+hipError_t launch_ci_dsr(const ConvArgs& a, hipStream_t s) {
+  using G = IGeo<W, sps_of<W, false>()>;
+  const int NI = (a.OCp / G::OT) * ((a.P + IL - 1) / IL), ncu = num_cus_i();
+  const dim3 grid(NI < ncu ? NI : ncu), block(INW * 64);
+  hipLaunchKernelGGL((conv3x3i_kernel<W, C, 0, true, false, true, true>), grid, block, 0, s, a);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+// conv2 of a downsampling block with the downsample residual computed in its
+// epilogue (conv3x3i_body DSR): int8 output, ReLU, no loaded residual; the
+// block input has C/2 channels at twice the resolution.
+hipError_t launch_conv3x3i_dsr(const ConvArgs& a, hipStream_t s) {
+  if (a.OCp != a.OC || a.C != a.OC || a.H != a.W || a.out_kind != 0 || !a.relu || a.res || !a.ds_x || !a.ds_w ||
+      !a.ds_alpha || !a.ds_beta || a.ds_C * 2 != a.C)
+    return hipErrorInvalidValue;
+  if ((long long)a.N * (2 * a.H) * (2 * a.W) * a.ds_C >= (1LL << 31)) return hipErrorInvalidValue;
+  switch (a.W) {
+    case 28: return a.C == 128 ? launch_ci_dsr<28, 128>(a, s) : hipErrorInvalidValue;
+    case 14: return a.C == 256 ? launch_ci_dsr<14, 256>(a, s) : hipErrorInvalidValue;
+    case 7: return a.C == 512 ? launch_ci_dsr<7, 512>(a, s) : hipErrorInvalidValue;
+  }
+  return hipErrorInvalidValue;
+}
 
 // e4m3 operands, same shapes and weight image layout (conv3x3w_pack of the codes).
 hipError_t launch_conv3x3i_f8(const ConvArgs& a, hipStream_t s) {
@@ -680,6 +850,7 @@ hipError_t launch_conv3x3i_f8(const ConvArgs& a, hipStream_t s) {
 
 // Weight image: conv3x3w_pack (wpack.cpp).
 hipError_t launch_conv3x3i(const ConvArgs& a, hipStream_t s) {
+  if (a.ds_x) return launch_conv3x3i_dsr(a, s);
   if (a.OCp != a.OC || a.C != a.OC || a.H != a.W) return hipErrorInvalidValue;
   switch (a.W) {
     case 28: return a.C == 128 ? launch_ci<28, 128>(a, s) : hipErrorInvalidValue;

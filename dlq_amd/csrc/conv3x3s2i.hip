@@ -577,6 +577,18 @@ hipError_t launch_j(const ConvArgs& a, const int8_t* w_ds, const float* al_ds, c
                          be_ds, y_ds);
     else
       hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, true, F8>), grid, block, 0, s, a, w_ds, al_ds, be_ds, y_ds);
+  } else if (!F8 && a.relu) {
+    // conv1 alone (the downsample computed by conv2, conv3x3i DSR): the
+    // v_cvt_pk_u8_f32 epilogue, and layer2.0's resident weights
+    if constexpr (OW == 28 && C == 64) {
+      if (a.OCp == JOT) {
+        hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, false, F8, true, true>), grid, block, 0, s, a, nullptr,
+                           nullptr, nullptr, nullptr);
+        return hipGetLastError();
+      }
+    }
+    hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, false, F8, false, true>), grid, block, 0, s, a, nullptr, nullptr,
+                       nullptr, nullptr);
   } else {
     hipLaunchKernelGGL((conv3x3s2i_kernel<OW, C, 0, false, F8>), grid, block, 0, s, a, nullptr, nullptr, nullptr,
                        nullptr);

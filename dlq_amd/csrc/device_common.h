@@ -88,6 +88,23 @@ __device__ __forceinline__ unsigned epi4_res_relu(const int* acc, const float* a
   return quant4_relu(y[0], y[1], y[2], y[3]);
 }
 
+// The downsample residual computed in place (conv3x3i.hip DSR): the 1x1/s2
+// downsample's accumulators `accd` requantised exactly as its own epilogue
+// would store them (rd = rne(clamp(fma(accd, ald, bed), -127, 127)), the int8
+// value held as a float: v_med3_f32 + v_rndne_f32), then used as conv2's
+// residual: y = fma(rd, r_s, fma(acc, al, be)) -> ReLU requantisation.
+// Bit-identical to storing rd as int8 and reading it back (epi4_res_relu).
+__device__ __forceinline__ unsigned epi4_dsr_relu(const int* acc, const float* al, const float* be, const int* accd,
+                                                  const float* ald, const float* bed, float r_s) {
+  float y[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float rd = __builtin_rintf(__builtin_amdgcn_fmed3f(__builtin_fmaf((float)accd[e], ald[e], bed[e]), -127.f, 127.f));
+    y[e] = __builtin_fmaf(rd, r_s, __builtin_fmaf((float)acc[e], al[e], be[e]));
+  }
+  return quant4_relu(y[0], y[1], y[2], y[3]);
+}
+
 // ---- fp8 (e4m3, OCP) helpers: DESIGN.md §3b, oracle.c ora_*_f8 ----------
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef int v8i __attribute__((ext_vector_type(8)));

@@ -11,7 +11,7 @@ namespace dlq {
 
 // Host-side knobs behind dlq_set_knob (capi.cpp): initialised once from the
 // environment when the library loads, never read from it on the hot path.
-extern std::atomic<int> g_knob_l1_grid, g_knob_head_split, g_knob_graph, g_knob_gemm_tile;
+extern std::atomic<int> g_knob_l1_grid, g_knob_head_split, g_knob_graph, g_knob_gemm_tile, g_knob_ds_split;
 extern std::atomic<unsigned> g_knob_gen;
 
 
@@ -31,6 +31,14 @@ struct ConvArgs {
   int relu;
   int out_kind;
   int dbg;  // ablation bits, read only by DLQ_ABLATION probe builds (tools/probe): 2 skip DMA, 4 skip epilogue
+  // Downsample residual of a downsampling block's conv2 (conv3x3i.hip, int8):
+  // the block input and the 1x1/s2 downsample, computed and requantised in
+  // conv2's epilogue; its int8 value is the residual (res == nullptr then).
+  const int8_t* ds_x;     // block input [N][2*OH][2*OW][ds_C], or nullptr
+  const int8_t* ds_w;     // downsample_pack image [OCp/128][ds_C/32][128][48]
+  const float* ds_alpha;  // [OCp], the downsample's output-grid units
+  const float* ds_beta;
+  int ds_C;
 };
 
 // Timing-ablation switches exist only in probe builds (tools/probe/*.hip
@@ -66,6 +74,9 @@ bool conv3x3w_shape(int C, int OC, int H, int W, int kH, int kW, int sH, int sW,
 size_t conv3x3w_packed_bytes(int OC, int C);
 void conv3x3w_pack(const int8_t* q_oihw, int OC, int IC, int C, int8_t* out);
 hipError_t launch_conv3x3i(const ConvArgs& a, hipStream_t s);
+// A downsampling block's conv2 with its 1x1/s2 downsample as the residual
+// (a.ds_*; int8, ReLU, a.res == nullptr): conv3x3i_kernel<..., DSR>.
+hipError_t launch_conv3x3i_dsr(const ConvArgs& a, hipStream_t s);
 // Stride-2 3x3 convs: the shapes and the 1x1/s2 downsample image (wpack.cpp),
 // conv1 in the wide image, and the 196-px item kernel (conv3x3s2i.hip) with
 // the optional fused downsample (w_ds == nullptr: conv only).

@@ -67,6 +67,52 @@ __global__ __launch_bounds__(256) void gap16_kernel(const int8_t* __restrict__ x
   }
 }
 
+// gap16_kernel for HW <= 8 * NPL (the ResNet-18 head: HW = 49, NPL = 7):
+// the same threads, sums and requantisation, but every pixel load of a
+// thread is issued before the first add, so the kernel waits for memory once
+// (gap16_kernel's loop keeps two loads in flight: four round trips at HW = 49).
+template <int NPL>
+__global__ __launch_bounds__(256) void gap16_once_kernel(const int8_t* __restrict__ x, int N, int C, int HW, float k,
+                                                         int8_t* __restrict__ y) {
+  const int tpi = (C / 16) * 8;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = (int)(t / tpi), r = (int)(t - (long)n * tpi);
+  const int pg = r & 7, cg = r >> 3;
+  const int8_t* src = x + (size_t)(n < N ? n : 0) * HW * C + cg * 16;
+  v4i v[NPL];
+#pragma unroll
+  for (int j = 0; j < NPL; ++j) {
+    const int i = pg + 8 * j;
+    v[j] = i < HW ? *(const v4i*)(src + (size_t)i * C) : v4i{0, 0, 0, 0};
+  }
+  int s[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s[i] = 0;
+#pragma unroll
+  for (int j = 0; j < NPL; ++j)
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) s[w * 4 + b] += (int)(signed char)(v[j][w] >> (8 * b));
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    s[i] += __shfl_xor(s[i], 1);
+    s[i] += __shfl_xor(s[i], 2);
+    s[i] += __shfl_xor(s[i], 4);
+  }
+  if (n < N && pg == 0) {
+    v4i o;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      unsigned u = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) u |= ((unsigned)sat_rne((float)s[w * 4 + b] * k) & 0xffu) << (8 * b);
+      o[w] = (int)u;
+    }
+    *(v4i*)(y + (size_t)n * C + cg * 16) = o;
+  }
+}
+
 // OUT: 0 int8 (optional ReLU), 1 fp32, 2 int32.
 template <int OUT>
 __global__ __launch_bounds__(64) void linear_kernel(const int8_t* __restrict__ x, int N, int K,
@@ -545,7 +591,13 @@ hipError_t launch_gap_fc(const int8_t* x, int N, int C, int HW, float k, const i
 
 hipError_t launch_gap(const int8_t* x, int N, int C, int HW, float k, int8_t* y, hipStream_t s) {
   const long total = (long)N * (C / 16) * 8;
-  hipLaunchKernelGGL(gap16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, N, C, HW, k, y);
+  const dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  if (HW <= 8)
+    hipLaunchKernelGGL(gap16_once_kernel<1>, grid, block, 0, s, x, N, C, HW, k, y);
+  else if (HW <= 56)
+    hipLaunchKernelGGL(gap16_once_kernel<7>, grid, block, 0, s, x, N, C, HW, k, y);
+  else
+    hipLaunchKernelGGL(gap16_kernel, grid, block, 0, s, x, N, C, HW, k, y);
   return hipGetLastError();
 }
 

@@ -223,6 +223,12 @@ float inv_scale(float s) { return 1.0f / s; }
 // launches (gap16_kernel + linear_kernel) instead of the fused gap_fc_kernel.
 bool head_split() { return g_knob_head_split.load(std::memory_order_relaxed) == 1; }
 
+// Knob "ds_split" (DLQ_DS_SPLIT=1, dlq_set_knob): a downsampling block's
+// 1x1/s2 downsample computed by its conv2 launch (conv3x3i DSR, stored where
+// conv2's output goes and read back as the residual) instead of fused into
+// the stride-2 conv1 launch (conv3x3s2i DS, the default).
+bool ds_split() { return g_knob_ds_split.load(std::memory_order_relaxed) == 1; }
+
 // conv2d_nchw_im2col_gemm + bn_launch (+ add_inplace + relu_forward) of the
 // reference, as one implicit-GEMM launch with the epilogue fused.
 int conv2d_nhwc_s8(const dlq_resnet18* m, const ConvLayer& c, const int8_t* x, int N, int H, int W,
@@ -292,6 +298,40 @@ int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N
     if (e != hipSuccess) return hip_fail(e, "block_l1 launch");
     *OH = H;
     *OW = W;
+    return DLQ_OK;
+  }
+  const ConvLayer* c2w = &m->convs[b.c2];
+  if (b.down && m->convs[b.ds].wf && ds_split() && conv3x3s2_shape(c1.Cstore, c1.OC, H, W, 3, 3, 2, 2, 1, 1) &&
+      wide_layout(c1.Cstore, c1.OC, H, W, 3, 3, 2, 2, 1, 1) &&
+      conv3x3w_shape(c2w->Cstore, c2w->OC, H / 2, W / 2, 3, 3, 1, 1, 1, 1) && c2w->Cstore == c1.OC &&
+      m->convs[b.ds].OC == c1.OC && 2 * c1.Cstore == c1.OC) {
+    // conv1 (3x3/s2) alone, then conv2 with the 1x1/s2 downsample computed
+    // and requantised in its epilogue as the residual (conv3x3i DSR): the
+    // downsample's output never goes to memory
+    const ConvLayer& ds = m->convs[b.ds];
+    const ConvLayer& c2 = *c2w;
+    dlq_conv_desc d{N, H, W, c1.Cstore, c1.OC, 3, 3, 2, 2, 1, 1};
+    if ((rc = mark(m, s, DLQ_FAM_S2DS))) return rc;
+    rc = dlq_conv2d_nhwc_s8(&d, in, c1.w, c1.alpha, c1.beta, nullptr, 0.f, 1, DLQ_OUT_S8, h, s);
+    if (rc) return rc;
+    h1 = out_dim(H, 3, 2, 1);
+    w1 = out_dim(W, 3, 2, 1);
+    if ((rc = mark(m, s, conv_family(c2, h1)))) return rc;
+    dlq_conv_desc d2{N, h1, w1, c2.Cstore, c2.OC, 3, 3, 1, 1, 1, 1};
+    ConvArgs a;
+    const float r_s = dlq::res_scale(m->scales.at(ds.site), m->scales.at(c2.site));
+    if ((rc = conv_args_checked(&d2, h, c2.w, c2.alpha, c2.beta, nullptr, r_s, 1, DLQ_OUT_S8, out, a))) return rc;
+    a.ds_x = in;
+    a.ds_w = ds.wf;
+    a.ds_alpha = ds.alpha;
+    a.ds_beta = ds.beta;
+    a.ds_C = c1.Cstore;
+    if (a.P) {
+      hipError_t e = launch_conv3x3i_dsr(a, s);
+      if (e != hipSuccess) return hip_fail(e, "conv2 + downsample residual launch");
+    }
+    *OH = h1;
+    *OW = w1;
     return DLQ_OK;
   }
   if (b.down && m->convs[b.ds].wf && conv3x3s2_shape(c1.Cstore, c1.OC, H, W, 3, 3, 2, 2, 1, 1) &&

@@ -74,6 +74,8 @@ _SIGS = {
     "dlq_pack_downsample_weights_s8": ([_vp, _i, _i, _i, _vp], _i),
     "dlq_block_l1_nhwc_s8": ([_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, C.c_float, _vp, _vp], _i),
     "dlq_conv2d_s2_ds_nhwc_s8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "dlq_conv2d_dsres_nhwc_s8": ([C.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_float, _vp, _vp],
+                                 _i),
     "dlq_stem_packed_bytes": ([], _sz),
     "dlq_pack_stem_weights_s8": ([_vp, _vp, _vp, _vp], _i),
     "dlq_stem_fused_s8": ([_vp, _i, _vp, _vp, _vp, _f, _vp, _vp], _i),

@@ -181,6 +181,26 @@ def conv2d_s2_ds_nhwc_s8(x: torch.Tensor, w_packed: torch.Tensor, alpha: torch.T
     return y, y_ds
 
 
+def conv2d_dsres_nhwc_s8(h: torch.Tensor, w_packed: torch.Tensor, alpha: torch.Tensor, beta: torch.Tensor,
+                         x_blk: torch.Tensor, w_ds: torch.Tensor, alpha_ds: torch.Tensor, beta_ds: torch.Tensor,
+                         res_scale: float) -> torch.Tensor:
+    """A downsampling block's conv2 (3x3/s1 + BN) with the residual = the
+    block input's 1x1/s2 downsample (+BN, requantised to int8) computed in the
+    same launch, + ReLU (include/dlq.h dlq_conv2d_dsres_nhwc_s8): NHWC h[N,H,W,C],
+    x_blk[N,2H,2W,C/2] -> int8 [N,H,W,C]."""
+    _dev(h, torch.int8)
+    _dev(x_blk, torch.int8)
+    N, H, W, Cc = h.shape
+    if tuple(x_blk.shape) != (N, 2 * H, 2 * W, Cc // 2):
+        raise ValueError(f"conv2d_dsres_nhwc_s8: block input {tuple(x_blk.shape)} does not match h {tuple(h.shape)}")
+    y = torch.empty_like(h)
+    d = ConvDesc(N, H, W, Cc, Cc, 3, 3, 1, 1, 1, 1)
+    check(lib.dlq_conv2d_dsres_nhwc_s8(C.byref(d), ptr(h), ptr(w_packed), ptr(alpha), ptr(beta), ptr(x_blk),
+                                       ptr(w_ds), ptr(alpha_ds), ptr(beta_ds), float(res_scale), ptr(y),
+                                       stream_handle()), "conv2d_dsres_nhwc_s8")
+    return y
+
+
 def block_l1_s8(x: torch.Tensor, w1: torch.Tensor, alpha1: torch.Tensor, beta1: torch.Tensor,
                 w2: torch.Tensor, alpha2: torch.Tensor, beta2: torch.Tensor, res_scale: float) -> torch.Tensor:
     """Fused layer1 basic block on NHWC int8 x[N,56,56,64] (see include/dlq.h

@@ -116,7 +116,12 @@ int dlq_pack_conv_weights_s8(const dlq_conv_desc* d, const int8_t* q_oihw, int I
  *   "head_split" (DLQ_HEAD_SPLIT) 1 = GAP and FC as two launches;
  *   "graph"      (DLQ_GRAPH)      1 = replay the forward as a hipGraph;
  *   "gemm_tile"  (DLQ_GEMM_TILE)  dlq_gemm_s8s8s32's tile, 0 = by shape,
- *                                 1 = 256 x 256, 2 = 256 x 128, 3 = 128 x 128.
+ *                                 1 = 256 x 256, 2 = 256 x 128, 3 = 128 x 128;
+ *   "ds_split"   (DLQ_DS_SPLIT)   1 = the engine computes a downsampling
+ *                                 block's 1x1/s2 downsample in its conv2
+ *                                 launch (dlq_conv2d_dsres_nhwc_s8) instead of
+ *                                 fusing it into the stride-2 conv1 launch
+ *                                 (dlq_conv2d_s2_ds_nhwc_s8, the default).
  * Returns DLQ_ERR_ARG for an unknown name. */
 int dlq_set_knob(const char* name, int value);
 int dlq_get_knob(const char* name, int* value);
@@ -216,6 +221,20 @@ int dlq_pack_downsample_weights_s8(const int8_t* q_ds, int OC, int IC, int C, in
 int dlq_conv2d_s2_ds_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
                              const float* alpha, const float* beta, const int8_t* w_ds, const float* alpha_ds,
                              const float* beta_ds, int8_t* y, int8_t* y_ds, void* stream);
+
+/* Downsampling BasicBlock back (infer_e2e.cu:177-186 conv2 + bn, :187-196
+ * the 1x1/s2 downsample conv + bn, :197-202 add + relu) in one launch: the
+ * 3x3/s1/p1 conv of h (d: C == OC, the layer2-4 shapes 28x28x128, 14x14x256,
+ * 7x7x512; w_packed from dlq_pack_conv_weights_s8) -> alpha/beta, plus the
+ * residual r = the block input x_blk[N][2H][2W][C/2]'s 1x1/s2 downsample
+ * (w_ds from dlq_pack_downsample_weights_s8, alpha_ds/beta_ds) requantised to
+ * int8 exactly as dlq_conv2d_s2_ds_nhwc_s8 stores y_ds, times res_scale ->
+ * ReLU -> int8 y.  Equals dlq_conv2d_s2_ds_nhwc_s8's y_ds fed to
+ * dlq_conv2d_nhwc_s8 as the residual, bit for bit; the downsample's output
+ * never goes to memory. */
+int dlq_conv2d_dsres_nhwc_s8(const dlq_conv_desc* d, const int8_t* h, const int8_t* w_packed, const float* alpha,
+                             const float* beta, const int8_t* x_blk, const int8_t* w_ds, const float* alpha_ds,
+                             const float* beta_ds, float res_scale, int8_t* y, void* stream);
 
 /* Fused layer1 basic block: int8 NHWC x[N][56][56][64] -> y (same shape) =
  * ReLU(requant(BN2(conv2(h)) + s_res * x)), h = ReLU(requant(BN1(conv1(x)))),

@@ -146,6 +146,104 @@ def test_s2_conv_with_fused_downsample_bitexact(gpu, C, H, N):
     assert np.array_equal(got_d, ref_d), f"downsample: {np.count_nonzero(got_d != ref_d)} mismatches"
 
 
+def _dsres_case(C, H, N, seed):
+    """A downsampling block's back half at conv2's resolution H (C channels):
+    block input x (C/2 @ 2H), conv2 input h, weights, scales and the oracle's
+    conv2 output with the downsample residual (infer_e2e.cu:177-202)."""
+    rng = np.random.default_rng(seed)
+    Ci = C // 2
+    x = rand_s8(rng, (N, Ci, 2 * H, 2 * H))
+    h = rand_s8(rng, (N, C, H, H))
+    w2, bn2 = rand_conv(rng, C, C, 3)
+    wd, bnd = rand_conv(rng, C, Ci, 1)
+    bnd[0][::5] *= -1
+    w2q, sw2 = O.quantize_weights_s8(w2)
+    wdq, swd = O.quantize_weights_s8(wd)
+    s_x, s_h, s_d, s_y = 0.03, 0.027, 0.06, 0.045  # a few % of both requantisations at a clamp
+    alpha, beta = O.fold_bn(s_h, sw2, bn2, s_y)
+    alpha_d, beta_d = O.fold_bn(s_x, swd, bnd, s_d)
+    r_s = O.res_scale(s_d, s_y)
+    return x, h, w2q, wdq, alpha, beta, alpha_d, beta_d, r_s
+
+
+def _dsres_gpu(x, h, w2q, wdq, alpha, beta, alpha_d, beta_d, r_s):
+    from dlq_amd import ops
+    C = h.shape[1]
+    hd, w2dev = _gpu_conv_inputs(h, w2q, 1, 1)
+    wds = _cuda(ops.pack_downsample_weights(wdq.reshape(C, C // 2), C // 2))
+    y = ops.conv2d_dsres_nhwc_s8(hd, w2dev, _cuda(alpha), _cuda(beta), _cuda(nchw_to_nhwc(x)), wds, _cuda(alpha_d),
+                                 _cuda(beta_d), r_s)
+    return nhwc_to_nchw(y.cpu().numpy())
+
+
+@pytest.mark.parametrize("C,H,N", [(128, 28, 3), (256, 14, 5), (512, 7, 37), (128, 28, 1), (512, 7, 9)])
+def test_conv2_with_downsample_residual_bitexact(gpu, C, H, N):
+    """layerX.0 conv2 (+BN) + the block's 1x1/s2 downsample (+BN, requantised)
+    computed in the same launch + ReLU == the oracle's downsample conv, its
+    int8 epilogue, and conv2's residual epilogue (infer_e2e.cu:177-202); ragged
+    batches (partial items, trash-line stores)."""
+    x, h, w2q, wdq, alpha, beta, alpha_d, beta_d, r_s = _dsres_case(C, H, N, C * 11 + N)
+    ref_d = O.epilogue_s8(O.conv_s8_acc(x, wdq, 2, 0), alpha_d, beta_d, None, 0.0, False)
+    ref = O.epilogue_s8(O.conv_s8_acc(h, w2q, 1, 1), alpha, beta, ref_d, r_s, True)
+    got = _dsres_gpu(x, h, w2q, wdq, alpha, beta, alpha_d, beta_d, r_s)
+    assert np.array_equal(got, ref), f"{np.count_nonzero(got != ref)} int8 mismatches"
+
+
+@pytest.mark.parametrize("C,H,N", [(128, 28, 90), (256, 14, 180), (512, 7, 360)])
+def test_conv2_with_downsample_residual_many_items(gpu, C, H, N):
+    """The downsample-residual epilogue when every workgroup walks several
+    items (the next item's DMA in flight during the epilogue's loads):
+    sampled images against the oracle, and the whole batch against the fused
+    stride-2 kernel's stored downsample fed to conv2 as a loaded residual."""
+    from dlq_amd import ops
+    x, h, w2q, wdq, alpha, beta, alpha_d, beta_d, r_s = _dsres_case(C, H, N, C + N)
+    got = _dsres_gpu(x, h, w2q, wdq, alpha, beta, alpha_d, beta_d, r_s)
+    for i in (0, 1, N // 2, N - 1):
+        ref_d = O.epilogue_s8(O.conv_s8_acc(x[i:i + 1], wdq, 2, 0), alpha_d, beta_d, None, 0.0, False)
+        ref = O.epilogue_s8(O.conv_s8_acc(h[i:i + 1], w2q, 1, 1), alpha, beta, ref_d, r_s, True)
+        assert np.array_equal(got[i:i + 1], ref), f"image {i}: {np.count_nonzero(got[i:i + 1] != ref)} mismatches"
+    # the two-launch form: downsample stored by the fused stride-2 kernel, read back as conv2's residual
+    Ci = C // 2
+    w1q, _ = O.quantize_weights_s8(rand_conv(np.random.default_rng(1), C, Ci, 3)[0])
+    xd, w1dev = _gpu_conv_inputs(x, w1q, 2, 1)
+    wds = _cuda(ops.pack_downsample_weights(wdq.reshape(C, Ci), Ci))
+    ones, zeros = _cuda(np.ones(C, np.float32)), _cuda(np.zeros(C, np.float32))
+    _, y_ds = ops.conv2d_s2_ds_nhwc_s8(xd, w1dev, ones, zeros, wds, _cuda(alpha_d), _cuda(beta_d))
+    hd, w2dev = _gpu_conv_inputs(h, w2q, 1, 1)
+    y2 = ops.conv2d_nhwc_s8(hd, w2dev, C, 3, 1, 1, _cuda(alpha), _cuda(beta), residual=y_ds, res_scale=r_s, relu=True)
+    two = nhwc_to_nchw(y2.cpu().numpy())
+    assert np.array_equal(got, two), f"{np.count_nonzero(got != two)} mismatches against the two-launch form"
+
+
+def test_conv2_with_downsample_residual_rejects_bad_shapes(gpu):
+    from dlq_amd import ops
+    from dlq_amd.lib import DLQError
+    h = torch.zeros((2, 28, 28, 128), dtype=torch.int8, device="cuda")
+    v = torch.zeros(128, dtype=torch.float32, device="cuda")
+    w = torch.zeros(1, dtype=torch.int8, device="cuda")
+    with pytest.raises(ValueError):  # block input of the wrong resolution
+        ops.conv2d_dsres_nhwc_s8(h, w, v, v, torch.zeros((2, 28, 28, 64), dtype=torch.int8, device="cuda"), w, v, v,
+                                 1.0)
+    h7 = torch.zeros((2, 7, 7, 256), dtype=torch.int8, device="cuda")  # not a wide stride-1 shape
+    with pytest.raises(DLQError):
+        ops.conv2d_dsres_nhwc_s8(h7, w, v, v, torch.zeros((2, 14, 14, 128), dtype=torch.int8, device="cuda"), w, v,
+                                 v, 1.0)
+
+
+def test_resnet18_downsample_residual_matches_fused_downsample(gpu, knobs):
+    """B=256 forward with the downsample computed in conv2's epilogue (default)
+    (knob ds_split = 1) == the default (the stride-2 launch stores it, conv2
+    reads it)."""
+    from dlq_amd.models import ResNet18Int8, synthetic_images
+    sd, scales = model_and_scales()
+    x = synthetic_images(256, seed=23).cuda()
+    model = ResNet18Int8(sd, scales, max_batch=256)
+    fused = model(x).cpu().numpy()
+    knobs("ds_split", 1)
+    split = model(x).cpu().numpy()
+    assert np.array_equal(split.view(np.int32), fused.view(np.int32))
+
+
 @pytest.mark.parametrize("C,H", [(128, 28), (256, 14), (512, 7)])
 @pytest.mark.parametrize("residual", [False, True])
 def test_wide_conv_no_relu_bitexact(gpu, C, H, residual):

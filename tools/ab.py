@@ -3,7 +3,7 @@
 usage: python tools/ab.py [--rounds 3] [--steps 20] LIB [LIB ...]
 Each LIB is a libdlq.so path (tools/build_variant.sh); 'base' = the in-tree
 dlq_amd/libdlq.so; LIB@VAR=VAL runs it with VAR=VAL in the environment (a
-knob's variable, e.g. base@DLQ_STEM=2).  Every round runs each build in its own process (the
+knob's variable, e.g. base@DLQ_DS_SPLIT=1 or base@DLQ_HEAD_SPLIT=1).  Every round runs each build in its own process (the
 library is chosen with DLQ_LIB_PATH), in rotating order, and prints the
 forward time and the per-family launch averages (hipEvents, rescaled to the
 timed forward as bench.py does).  With --check the first build's logits are
@@ -16,6 +16,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# environment variables libdlq.so reads (capi.cpp knobs) or the child reads
+KNOWN_VARS = {"DLQ_L1_GRID", "DLQ_HEAD_SPLIT", "DLQ_GRAPH", "DLQ_GEMM_TILE", "DLQ_DS_SPLIT", "DLQ_LIB_PATH"}
 
 CHILD = r"""
 import json, os, sys, time, torch, numpy as np
@@ -80,6 +82,9 @@ def main():
             path, _, kv = lib.partition("@")
             if kv:
                 k, _, v = kv.partition("=")
+                if k not in KNOWN_VARS:
+                    print(f"warning: {k} is not a libdlq knob variable ({', '.join(sorted(KNOWN_VARS))}): "
+                          f"{lib} runs with it set but nothing reads it", flush=True)
                 env[k] = v
             if path != "base":
                 env["DLQ_LIB_PATH"] = os.path.abspath(path)
