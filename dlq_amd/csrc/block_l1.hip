@@ -106,6 +106,7 @@ struct BlockArgs {
   const float* b2;
   float s_res;  // residual scale in conv2's output-grid units
   int N;
+  Prefetch pf;  // the next launch's first weight stages (engine forwards)
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -709,6 +710,9 @@ __device__ __forceinline__ void block_l1_sp_role(const BlockArgs& a, int8_t* lds
     if constexpr (SECOND) __builtin_amdgcn_s_setprio(0);
     if constexpr (!SECOND) {
       dma_some(8);
+      // the last phase has no conv1 jobs: the idle conv1 waves pull the next
+      // launch's first weight stages into the input ring (read by nothing now)
+      if (lastp) prefetch_next(a.pf, wave, 4, lds32 + OFF_IN);
       wait_vm0();  // this phase's DMA has landed
     }
     BT(2);
@@ -754,9 +758,9 @@ bool block_l1_shape(int C, int OC, int H, int W) { return C == LC && OC == LC &&
 
 hipError_t launch_block_l1(const int8_t* x, int N, const int8_t* w1, const float* a1, const float* b1,
                            const int8_t* w2, const float* a2, const float* b2, float s_res, int8_t* y,
-                           hipStream_t s, bool f8) {
+                           hipStream_t s, bool f8, const Prefetch* pf) {
   if (N <= 0) return hipSuccess;
-  BlockArgs a{x, y, w1, w2, a1, b1, a2, b2, s_res, N};
+  BlockArgs a{x, y, w1, w2, a1, b1, a2, b2, s_res, N, pf ? *pf : Prefetch{}};
   int grid = num_cus_b();
   {  // knob "l1_grid" (DLQ_L1_GRID, dlq_set_knob): several images per workgroup
     const int g = g_knob_l1_grid.load(std::memory_order_relaxed);

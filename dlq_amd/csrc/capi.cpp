@@ -125,6 +125,7 @@ std::atomic<int> g_knob_head_split{env_int("DLQ_HEAD_SPLIT")};
 std::atomic<int> g_knob_graph{env_int("DLQ_GRAPH")};
 std::atomic<int> g_knob_gemm_tile{env_int("DLQ_GEMM_TILE")};
 std::atomic<int> g_knob_ds_split{env_int("DLQ_DS_SPLIT")};
+std::atomic<int> g_knob_prefetch{env_int("DLQ_PREFETCH")};
 // bumped by every dlq_set_knob: a forward captured as a hipGraph under other
 // knob values (head_split, l1_grid change its launches) is captured again
 std::atomic<unsigned> g_knob_gen{0};
@@ -137,6 +138,7 @@ std::atomic<int>* knob(const char* name) {
   if (!std::strcmp(name, "graph")) return &g_knob_graph;
   if (!std::strcmp(name, "gemm_tile")) return &g_knob_gemm_tile;
   if (!std::strcmp(name, "ds_split")) return &g_knob_ds_split;
+  if (!std::strcmp(name, "prefetch")) return &g_knob_prefetch;
   return nullptr;
 }
 }  // namespace
@@ -276,16 +278,25 @@ extern "C" {
 int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
                        const float* alpha, const float* beta, const int8_t* residual,
                        float res_scale, int relu, int out_kind, void* y, void* stream) {
+  return conv2d_nhwc_s8_pf(d, x, w_packed, alpha, beta, residual, res_scale, relu, out_kind, y, stream, nullptr);
+}
+
+}  // extern "C"
+int dlq::conv2d_nhwc_s8_pf(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
+                           const float* beta, const int8_t* residual, float res_scale, int relu, int out_kind,
+                           void* y, void* stream, const Prefetch* pf) {
   ConvArgs a;
   bool wide = false;
   int rc = conv_args(d, x, w_packed, alpha, beta, residual, res_scale, relu, out_kind, y, a, wide);
   if (rc) return rc;
   if (a.P == 0) return DLQ_OK;
+  if (pf && wide) a.pf = *pf;
   hipError_t e = !wide ? launch_conv(a, (hipStream_t)stream)
                  : a.sH == 2 ? launch_conv3x3s2i(a, nullptr, nullptr, nullptr, nullptr, (hipStream_t)stream)
                              : launch_conv3x3i(a, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d launch: ") + hipGetErrorString(e));
 }
+extern "C" {
 
 size_t dlq_downsample_packed_bytes(int OC, int C) {
   return (OC > 0 && C > 0 && C % 32 == 0) ? downsample_packed_bytes(OC, C) : 0;
@@ -301,6 +312,13 @@ int dlq_pack_downsample_weights_s8(const int8_t* q, int OC, int IC, int C, int8_
 int dlq_conv2d_s2_ds_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed,
                              const float* alpha, const float* beta, const int8_t* w_ds, const float* alpha_ds,
                              const float* beta_ds, int8_t* y, int8_t* y_ds, void* stream) {
+  return conv2d_s2_ds_nhwc_s8_pf(d, x, w_packed, alpha, beta, w_ds, alpha_ds, beta_ds, y, y_ds, stream, nullptr);
+}
+
+}  // extern "C"
+int dlq::conv2d_s2_ds_nhwc_s8_pf(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
+                                 const float* beta, const int8_t* w_ds, const float* alpha_ds, const float* beta_ds,
+                                 int8_t* y, int8_t* y_ds, void* stream, const Prefetch* pf) {
   if (!d || !conv3x3s2_shape(DLQ_DESC_GEOM(d)))
     return fail(DLQ_ERR_ARG, "conv2d_s2_ds: needs a 3x3/s2/p1 C->2C conv at 56x56x64, 28x28x128 or 14x14x256");
   if (!w_ds || !alpha_ds || !beta_ds || !y_ds) return fail(DLQ_ERR_ARG, "conv2d_s2_ds: null pointer");
@@ -309,9 +327,11 @@ int dlq_conv2d_s2_ds_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8
   int rc = conv_args(d, x, w_packed, alpha, beta, nullptr, 0.f, 1, DLQ_OUT_S8, y, a, wide);
   if (rc) return rc;
   if (a.P == 0) return DLQ_OK;
+  if (pf) a.pf = *pf;
   hipError_t e = launch_conv3x3s2i(a, w_ds, alpha_ds, beta_ds, y_ds, (hipStream_t)stream);
   return e == hipSuccess ? DLQ_OK : fail(DLQ_ERR_LAUNCH, std::string("conv2d_s2_ds launch: ") + hipGetErrorString(e));
 }
+extern "C" {
 
 int dlq_conv2d_dsres_nhwc_s8(const dlq_conv_desc* d, const int8_t* h, const int8_t* w_packed, const float* alpha,
                              const float* beta, const int8_t* x_blk, const int8_t* w_ds, const float* alpha_ds,

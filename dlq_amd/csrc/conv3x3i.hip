@@ -485,6 +485,9 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
     // (fp8: one instantiation with the runtime test -- two spill its registers)
     const bool more = decltype(more_c)::value && (!F8 || s + 1 < nst);
     if (more && loader) prep_for(s + 1);
+    // the launch's last stage issues no DMA of its own: pull the next
+    // launch's first weight stages (engine forwards) into the idle slot
+    if constexpr (!decltype(more_c)::value && !F8) prefetch_next(a.pf, wave, INW, lds_addr32(lds) + ((s + 1) & 1) * G::SLOT);
 
     if (j == 0) {
       item_of(li, cur_ot, cur_p0);

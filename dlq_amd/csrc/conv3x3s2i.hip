@@ -387,6 +387,9 @@ __device__ __forceinline__ void s2i_body(const ConvArgs& a, const int8_t* w_ds, 
     // (fp8: one instantiation with the runtime test -- two spill its registers)
     const bool more = decltype(more_c)::value && (!F8 || s + 1 < nst);
     if (more) prep_for(s + 1);
+    // the launch's last stage issues no DMA of its own: pull the next
+    // launch's first weight stages (engine forwards) into the idle patch slot
+    if constexpr (!decltype(more_c)::value && !F8) prefetch_next(a.pf, wave, JNW, lds32 + ((s + 1) & 1) * G::SLOT + G::OFF_P);
     if (j == 0) {
       item_of(li, cur_ot, cur_p0);
 #pragma unroll

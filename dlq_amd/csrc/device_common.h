@@ -279,6 +279,28 @@ __device__ __forceinline__ void glds16_saddr_m(const void* base, unsigned voff, 
       : "memory");
 }
 
+// The next launch's weight regions (ConvArgs::pf) pulled towards the CUs:
+// one 1 KiB LDS-DMA piece per wave of the grid (pieces numbered across both
+// regions, spread over every wave), landing in an LDS area nobody reads (an
+// idle ring slot), so no VGPR is written behind the compiler's back.  The
+// launch's own counted waits see these as older VM ops: issue them where
+// every later wait may cover them (a last stage, no DMA after).
+__device__ __forceinline__ void prefetch_next(const Prefetch& pf, int wave, int nw, unsigned lds_dummy) {
+  const int lane = threadIdx.x & 63;
+  int q = blockIdx.x * nw + wave;
+  const int G = gridDim.x * nw;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (!pf.p[r]) continue;
+    const int per = pf.len[r] >> 10, tot = pf.n[r] * per;
+    for (; q < tot; q += G) {
+      const int blk = q / per, off = (q - blk * per) * 1024;
+      glds16_asm((const int8_t*)pf.p[r] + (size_t)blk * pf.stride[r] + off + lane * 16, lds_dummy);
+    }
+    q -= tot;
+  }
+}
+
 // LDS byte address of a __shared__ pointer (for M0).
 __device__ __forceinline__ unsigned lds_addr32(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;

@@ -11,9 +11,19 @@ namespace dlq {
 
 // Host-side knobs behind dlq_set_knob (capi.cpp): initialised once from the
 // environment when the library loads, never read from it on the hot path.
-extern std::atomic<int> g_knob_l1_grid, g_knob_head_split, g_knob_graph, g_knob_gemm_tile, g_knob_ds_split;
+extern std::atomic<int> g_knob_l1_grid, g_knob_head_split, g_knob_graph, g_knob_gemm_tile, g_knob_ds_split,
+    g_knob_prefetch;
 extern std::atomic<unsigned> g_knob_gen;
 
+
+// Weight regions of the NEXT launch of a forward, read (into the memory-side
+// cache and L2) by the current launch's last stage so that the next launch's
+// first stages do not start from HBM: up to two regions of n blocks of len
+// bytes (a multiple of 1 KiB), stride bytes apart.  p == nullptr: none.
+struct Prefetch {
+  const void* p[2];
+  int n[2], stride[2], len[2];
+};
 
 // Conv launch parameters (device view).  Activations are NHWC int8.
 struct ConvArgs {
@@ -39,6 +49,7 @@ struct ConvArgs {
   const float* ds_alpha;  // [OCp], the downsample's output-grid units
   const float* ds_beta;
   int ds_C;
+  Prefetch pf;  // the next launch's first weight blocks (engine forwards only)
 };
 
 // Timing-ablation switches exist only in probe builds (tools/probe/*.hip
@@ -90,12 +101,13 @@ hipError_t launch_conv3x3s2i(const ConvArgs& a, const int8_t* w_ds, const float*
 bool block_l1_shape(int C, int OC, int H, int W);
 hipError_t launch_block_l1(const int8_t* x, int N, const int8_t* w1, const float* a1, const float* b1,
                            const int8_t* w2, const float* a2, const float* b2, float s_res, int8_t* y,
-                           hipStream_t s, bool f8 = false);
+                           hipStream_t s, bool f8 = false, const struct Prefetch* pf = nullptr);
 // Fused stem (stem.hip): quantise + conv1 7x7/s2 + BN/ReLU/requant + maxpool.
 size_t stem_packed_bytes();
 void pack_stem_weights(const int8_t* q_oihw, const float* alpha, int8_t* out, float* alpha_abs);
 hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float* alpha, const float* beta,
-                             float inv_s, int8_t* y, hipStream_t s, bool f8 = false);
+                             float inv_s, int8_t* y, hipStream_t s, bool f8 = false,
+                             const struct Prefetch* pf = nullptr);
 void pack_stem_weights_f8(const uint8_t* q_oihw, const float* alpha, uint8_t* out, float* alpha_abs);
 hipError_t launch_quantize_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cout,
                                         float inv_s, int8_t* y, hipStream_t s);
@@ -179,6 +191,14 @@ namespace dlq {
 int conv_args_checked(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
                       const float* beta, const int8_t* residual, float res_scale, int relu, int out_kind, void* y,
                       ConvArgs& a);
+// dlq_conv2d_nhwc_s8 / dlq_conv2d_s2_ds_nhwc_s8 with the next launch's weight
+// regions (Prefetch; nullptr = none) for the engine's forward.
+int conv2d_nhwc_s8_pf(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
+                      const float* beta, const int8_t* residual, float res_scale, int relu, int out_kind, void* y,
+                      void* stream, const Prefetch* pf);
+int conv2d_s2_ds_nhwc_s8_pf(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
+                            const float* beta, const int8_t* w_ds, const float* alpha_ds, const float* beta_ds,
+                            int8_t* y, int8_t* y_ds, void* stream, const Prefetch* pf);
 
 inline int out_dim(int in, int k, int s, int p) { return (in + 2 * p - k) / s + 1; }
 

@@ -229,18 +229,43 @@ bool head_split() { return g_knob_head_split.load(std::memory_order_relaxed) == 
 // the stride-2 conv1 launch (conv3x3s2i DS, the default).
 bool ds_split() { return g_knob_ds_split.load(std::memory_order_relaxed) == 1; }
 
+// Knob "prefetch" (DLQ_PREFETCH): 0 = default on, -1 = off.  Each wide /
+// stride-2 conv launch's last stage reads the next launch's first weight
+// stages (Prefetch, device_common.h prefetch_next).
+bool prefetch_on() { return g_knob_prefetch.load(std::memory_order_relaxed) >= 0; }
+
 // conv2d_nchw_im2col_gemm + bn_launch (+ add_inplace + relu_forward) of the
 // reference, as one implicit-GEMM launch with the epilogue fused.
 int conv2d_nhwc_s8(const dlq_resnet18* m, const ConvLayer& c, const int8_t* x, int N, int H, int W,
                    const int8_t* residual, float res_scale, bool relu, int8_t* y, hipStream_t s,
-                   int* OH, int* OW) {
+                   int* OH, int* OW, const Prefetch* pf = nullptr) {
   dlq_conv_desc d{N, H, W, c.Cstore, c.OC, c.k, c.k, c.s, c.s, c.p, c.p};
   *OH = out_dim(H, c.k, c.s, c.p);
   *OW = out_dim(W, c.k, c.s, c.p);
   // alpha/beta are already in this conv's output-grid units (prepare); the
   // residual's scale is converted the same way.
   const float r_s = residual ? dlq::res_scale(res_scale, m->scales.at(c.site)) : 0.f;
-  return dlq_conv2d_nhwc_s8(&d, x, c.w, c.alpha, c.beta, residual, r_s, relu ? 1 : 0, DLQ_OUT_S8, y, s);
+  return conv2d_nhwc_s8_pf(&d, x, c.w, c.alpha, c.beta, residual, r_s, relu ? 1 : 0, DLQ_OUT_S8, y, s, pf);
+}
+
+// The first weight stages a launch of conv `c` (input H x H) streams: the
+// wide image's first four 32-channel slices of every 128-channel block (and
+// of the fused downsample's image), or none for other layouts.
+Prefetch conv_prefetch(const ConvLayer& c, int H, const ConvLayer* ds = nullptr) {
+  Prefetch pf{};
+  if (!(c.k == 3 && wide_layout(c.Cstore, c.OC, H, H, 3, 3, c.s, c.s, 1, 1))) return pf;
+  const int NS = c.Cstore / 32, ns = NS < 4 ? NS : 4, nb = packed_oc(c.OC) / 128;
+  pf.p[0] = c.w;
+  pf.n[0] = nb;
+  pf.stride[0] = NS * 128 * 304;
+  pf.len[0] = ns * 128 * 304;
+  if (ds && ds->wf) {
+    pf.p[1] = ds->wf;
+    pf.n[1] = nb;
+    pf.stride[1] = NS * 128 * 48;
+    pf.len[1] = ns * 128 * 48;
+  }
+  return pf;
 }
 
 int mark(dlq_resnet18* m, hipStream_t s, int family) {
@@ -278,11 +303,26 @@ bool fused_l1_block(const dlq_resnet18* m, const Block& b, int H, int W) {
          !wide_layout(c1.Cstore, c1.OC, H, W, 3, 3, 1, 1, 1, 1);
 }
 
+// The first weights the first launch of block `b` (input H x H) reads: the
+// fused layer1 block's two weight images, or its first conv's stages.
+Prefetch block_prefetch(const dlq_resnet18* m, const Block& b, int H) {
+  if (fused_l1_block(m, b, H, H)) {
+    Prefetch pf{};
+    const int len = (int)packed_bytes(64, 64, 3, 3);
+    pf.p[0] = m->convs[b.c1].w;
+    pf.p[1] = m->convs[b.c2].w;
+    pf.n[0] = pf.n[1] = 1;
+    pf.len[0] = pf.len[1] = len;
+    return pf;
+  }
+  return conv_prefetch(m->convs[b.c1], H, b.down ? &m->convs[b.ds] : nullptr);
+}
+
 // basic_block_forward (infer_e2e.cu:156-203): conv-bn-relu, conv-bn,
 // identity | 1x1 downsample-bn, add, relu -- three launches at most.
 int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N, int H,
                         int W, int8_t* h, int8_t* dsb, int8_t* out, hipStream_t s, int* OH,
-                        int* OW) {
+                        int* OW, const Prefetch* next = nullptr) {
   int h1, w1, h2, w2;
   const ConvLayer& c1 = m->convs[b.c1];
   const int8_t* skip = in;
@@ -294,7 +334,8 @@ int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N
     const ConvLayer& c2 = m->convs[b.c2];
     if ((rc = mark(m, s, DLQ_FAM_L1))) return rc;
     const float r_s = dlq::res_scale(s_skip, m->scales.at(c2.site));
-    hipError_t e = launch_block_l1(in, N, c1.w, c1.alpha, c1.beta, c2.w, c2.alpha, c2.beta, r_s, out, s);
+    hipError_t e = launch_block_l1(in, N, c1.w, c1.alpha, c1.beta, c2.w, c2.alpha, c2.beta, r_s, out, s, false,
+                                   prefetch_on() ? next : nullptr);
     if (e != hipSuccess) return hip_fail(e, "block_l1 launch");
     *OH = H;
     *OW = W;
@@ -340,7 +381,9 @@ int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N
     const ConvLayer& ds = m->convs[b.ds];
     dlq_conv_desc d{N, H, W, c1.Cstore, c1.OC, 3, 3, 2, 2, 1, 1};
     if ((rc = mark(m, s, DLQ_FAM_S2DS))) return rc;
-    rc = dlq_conv2d_s2_ds_nhwc_s8(&d, in, c1.w, c1.alpha, c1.beta, ds.wf, ds.alpha, ds.beta, h, dsb, s);
+    const Prefetch pf2 = conv_prefetch(m->convs[b.c2], out_dim(H, 3, 2, 1));
+    rc = conv2d_s2_ds_nhwc_s8_pf(&d, in, c1.w, c1.alpha, c1.beta, ds.wf, ds.alpha, ds.beta, h, dsb, s,
+                                 prefetch_on() ? &pf2 : nullptr);
     if (rc) return rc;
     h1 = out_dim(H, 3, 2, 1);
     w1 = out_dim(W, 3, 2, 1);
@@ -348,7 +391,9 @@ int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N
     s_skip = m->scales.at(ds.site);
   } else {
     if ((rc = mark(m, s, conv_family(c1, H)))) return rc;
-    rc = conv2d_nhwc_s8(m, c1, in, N, H, W, nullptr, 0.f, true, h, s, &h1, &w1);
+    const Prefetch pf2 = conv_prefetch(m->convs[b.c2], out_dim(H, 3, c1.s, 1));
+    rc = conv2d_nhwc_s8(m, c1, in, N, H, W, nullptr, 0.f, true, h, s, &h1, &w1,
+                        !b.down && prefetch_on() ? &pf2 : nullptr);
     if (rc) return rc;
     if (b.down) {
       int hd, wd;
@@ -361,7 +406,8 @@ int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N
     }
   }
   if ((rc = mark(m, s, conv_family(m->convs[b.c2], h1)))) return rc;
-  rc = conv2d_nhwc_s8(m, m->convs[b.c2], h, N, h1, w1, skip, s_skip, true, out, s, &h2, &w2);
+  rc = conv2d_nhwc_s8(m, m->convs[b.c2], h, N, h1, w1, skip, s_skip, true, out, s, &h2, &w2,
+                      prefetch_on() ? next : nullptr);
   *OH = h2;
   *OW = w2;
   return rc;
@@ -957,8 +1003,12 @@ int forward_pass(dlq_resnet18* m, const float* x, int B, float* logits, hipStrea
   // 0+1) fused stem: quantise + conv 7x7/s2 + BN + ReLU + maxpool 3x3/s2
   //      (infer_e2e.cu:255-293) in one launch
   if ((rc = mark(m, s, DLQ_FAM_STEM))) return rc;
-  rc = dlq_stem_fused_s8(x, B, m->stem_w, m->stem_alpha, st.beta, inv_scale(m->scales.at("input")), cur, stream);
-  if (rc) return rc;
+  if (B > 0) {  // (the stem's C-ABI entry, dlq_stem_fused_s8, with the next launch's prefetch)
+    const Prefetch pf = block_prefetch(m, m->blocks[0], 56);
+    hipError_t e = launch_stem_fused(x, B, m->stem_w, m->stem_alpha, st.beta, inv_scale(m->scales.at("input")), cur,
+                                     s, false, prefetch_on() ? &pf : nullptr);
+    if (e != hipSuccess) return hip_fail(e, "stem launch");
+  }
   if (record && (rc = record_stage(m, "stem_pool", cur, nB * H * W * 64, s))) return rc;
   // 2-5) layer1..layer4 (:300-415)
   for (size_t bi = 0; bi < m->blocks.size(); ++bi) {
@@ -968,7 +1018,18 @@ int forward_pass(dlq_resnet18* m, const float* x, int B, float* logits, hipStrea
     for (int i = 0; i < 4; ++i)
       if (i != ci && k < 3) fi[k++] = i;
     int OH, OW;
-    rc = basic_block_forward(m, b, cur, B, H, W, bufp(fi[0]), bufp(fi[1]), bufp(fi[2]), s, &OH, &OW);
+    // the launch after this block: the next block's first launch, or the
+    // head's FC weights
+    Prefetch next{};
+    if (bi + 1 < m->blocks.size()) {
+      next = block_prefetch(m, m->blocks[bi + 1], b.stride == 2 ? out_dim(H, 3, 2, 1) : H);
+    } else {
+      next.p[0] = m->fc_w;
+      next.n[0] = 1;
+      next.stride[0] = 0;
+      next.len[0] = (int)(packed_bytes(1000, 512, 1, 1) & ~(size_t)1023);
+    }
+    rc = basic_block_forward(m, b, cur, B, H, W, bufp(fi[0]), bufp(fi[1]), bufp(fi[2]), s, &OH, &OW, &next);
     if (rc) return rc;
     ci = fi[2];
     cur = bufp(ci);

@@ -110,6 +110,7 @@ struct StemArgs {
   int8_t* y;           // [N][56][56][64]
   float inv_s;         // 1 / input scale
   int N, nb, R;        // batch, bands per image, pooled rows per band
+  Prefetch pf;         // the next launch's weights (engine forwards)
 };
 
 
@@ -521,7 +522,8 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
 constexpr int S2W = 4;                          // waves: one per column quarter
 constexpr int STG2 = 64 * 16;                   // per wave: [64 oc][16 px] bytes
 constexpr int OFF_STAGE2 = OFF_CR + CR_SLOTS * CR_ROW;
-constexpr int LDS_STEM2 = OFF_STAGE2 + S2W * STG2;
+constexpr int OFF_PF2 = OFF_STAGE2 + S2W * STG2;  // 1 KiB nobody reads: the prefetch pieces' destination
+constexpr int LDS_STEM2 = OFF_PF2 + 1024;
 static_assert(2 * LDS_STEM2 <= 160 * 1024, "two workgroups per CU");
 
 __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
@@ -557,6 +559,9 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
 
   int item0, n_my;
   xcd_chunk(nitems, item0, n_my);
+  // the next launch's weights (the first layer1 block's), pulled towards the
+  // CUs while this launch runs; the item loop's vmcnt(0) waits cover them
+  prefetch_next(a.pf, q, S2W, lds32 + OFF_PF2);
   for (int li = 0; li < n_my; ++li) {
     const int item = xcd_item(item0, li);
     const int n = item / a.nb, band = item - n * a.nb;
@@ -799,13 +804,13 @@ void pack_stem_weights_f8(const uint8_t* q, const float* alpha, uint8_t* out, fl
 }
 
 hipError_t launch_stem_fused(const float* x, int N, const int8_t* w, const float* alpha, const float* beta,
-                             float inv_s, int8_t* y, hipStream_t s, bool f8) {
+                             float inv_s, int8_t* y, hipStream_t s, bool f8, const Prefetch* pf) {
   const int ncu = num_cus_stem();
   int nb = (2 * ncu + N - 1) / N;  // bands per image so that every CU gets two co-resident items
   nb = nb < 1 ? 1 : (nb > 14 ? 14 : nb);
   const int R = (56 + nb - 1) / nb;
   nb = (56 + R - 1) / R;
-  StemArgs a{x, w, alpha, beta, y, inv_s, N, nb, R};
+  StemArgs a{x, w, alpha, beta, y, inv_s, N, nb, R, pf && !f8 ? *pf : Prefetch{}};
   const int items = N * nb, grid = items < 2 * ncu ? items : 2 * ncu;
   if (f8)
     hipLaunchKernelGGL(stem_fused_kernel<true>, dim3(grid), dim3(SNW * 64), 0, s, a);
