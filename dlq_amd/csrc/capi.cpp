@@ -126,6 +126,7 @@ std::atomic<int> g_knob_graph{env_int("DLQ_GRAPH")};
 std::atomic<int> g_knob_gemm_tile{env_int("DLQ_GEMM_TILE")};
 std::atomic<int> g_knob_ds_split{env_int("DLQ_DS_SPLIT")};
 std::atomic<int> g_knob_prefetch{env_int("DLQ_PREFETCH")};
+std::atomic<int> g_knob_gap_epi{env_int("DLQ_GAP_EPI")};
 // bumped by every dlq_set_knob: a forward captured as a hipGraph under other
 // knob values (head_split, l1_grid change its launches) is captured again
 std::atomic<unsigned> g_knob_gen{0};
@@ -139,6 +140,7 @@ std::atomic<int>* knob(const char* name) {
   if (!std::strcmp(name, "gemm_tile")) return &g_knob_gemm_tile;
   if (!std::strcmp(name, "ds_split")) return &g_knob_ds_split;
   if (!std::strcmp(name, "prefetch")) return &g_knob_prefetch;
+  if (!std::strcmp(name, "gap_epi")) return &g_knob_gap_epi;
   return nullptr;
 }
 }  // namespace
@@ -284,13 +286,18 @@ int dlq_conv2d_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_
 }  // extern "C"
 int dlq::conv2d_nhwc_s8_pf(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
                            const float* beta, const int8_t* residual, float res_scale, int relu, int out_kind,
-                           void* y, void* stream, const Prefetch* pf) {
+                           void* y, void* stream, const Prefetch* pf, int8_t* gap_y, float gap_k) {
   ConvArgs a;
   bool wide = false;
   int rc = conv_args(d, x, w_packed, alpha, beta, residual, res_scale, relu, out_kind, y, a, wide);
   if (rc) return rc;
   if (a.P == 0) return DLQ_OK;
   if (pf && wide) a.pf = *pf;
+  if (gap_y) {
+    if (!wide || a.sH != 1) return fail(DLQ_ERR_STATE, "conv2d: the pooled output needs the wide 7x7x512 conv");
+    a.gap_y = gap_y;
+    a.gap_k = gap_k;
+  }
   hipError_t e = !wide ? launch_conv(a, (hipStream_t)stream)
                  : a.sH == 2 ? launch_conv3x3s2i(a, nullptr, nullptr, nullptr, nullptr, (hipStream_t)stream)
                              : launch_conv3x3i(a, (hipStream_t)stream);
@@ -337,7 +344,8 @@ int dlq_conv2d_dsres_nhwc_s8(const dlq_conv_desc* d, const int8_t* h, const int8
                              const float* beta, const int8_t* x_blk, const int8_t* w_ds, const float* alpha_ds,
                              const float* beta_ds, float res_scale, int8_t* y, void* stream) {
   if (!d || !conv3x3w_shape(DLQ_DESC_GEOM(d)))
-    return fail(DLQ_ERR_ARG, "conv2d_dsres: needs a 3x3/s1/p1 C->C conv at 28x28x128, 14x14x256 or 7x7x512");
+    return fail(DLQ_ERR_ARG, "conv2d_dsres: needs a 3x3/s1/p1 C->C conv at 28x28x128 or 14x14x256");
+  if (d->H == 7) return fail(DLQ_ERR_ARG, "conv2d_dsres: 7x7x512 is not supported (no LDS for the pixel region)");
   if (!x_blk || !w_ds || !alpha_ds || !beta_ds) return fail(DLQ_ERR_ARG, "conv2d_dsres: null pointer");
   ConvArgs a;
   bool wide = false;

@@ -106,6 +106,23 @@ constexpr int sps_of() {
   return W == 7 && !F8 ? 2 : 1;
 }
 
+// The DSR LDS regions past the ring and alpha/beta (conv3x3i_body DSR): the
+// downsample's alpha / beta of the item's 128 channels (1 KiB), then the
+// item's block-input pixels, NCH 16-byte chunks each, chunk c of pixel lp at
+// unit lp * NCH + (c ^ swz(lp)) -- a B-fragment ds_read_b128's 16-lane group
+// (16 of a tile's consecutive pixels, one chunk) then covers 16 distinct bank
+// quads.
+template <int W, int C>
+struct DsrGeo {
+  using G = IGeo<W, 1>;
+  static constexpr int NCH = C / 32;                 // 16-byte chunks per block-input pixel (C/2 channels)
+  static constexpr int NPD = (IL * NCH + 63) / 64;   // LDS-DMA pieces of the pixel region
+  static constexpr int OFF_DAB = G::OFF_AB + 2 * C * 4;
+  static constexpr int OFF_DS = OFF_DAB + 1024;
+  static constexpr int LDS_END = OFF_DS + NPD * 1024;
+  static __device__ __forceinline__ int swz(int lp) { return NCH == 4 ? (lp >> 2) & 3 : (lp >> 1) & 7; }
+};
+
 // Wave -> (oc tile, first px tile, px tile count).  MT = 4: SIMD pair (w, w+4)
 // = oc tile w&3, tiles [0,7) and [7,13).  MT = 2: oc tile w&1, tile groups
 // [0,4) [4,7) [7,10) [10,13) by w>>1, so the pair (w, w+4) owns 7 or 6.
@@ -156,20 +173,6 @@ __device__ __forceinline__ void wait_vm_tie_frags(v4i (&x)[K]) {
                  : "n"(N)
                  : "memory");
 }
-// register ties without a wait (after a runtime-count wait_vm)
-template <int K>
-__device__ __forceinline__ void tie_frags(v4i (&x)[K]) {
-#pragma unroll
-  for (int i = 0; i < K; ++i) asm volatile("" : "+v"(x[i]));
-}
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for_i(F& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for_i<I + 1, N>(f);
-  }
-}
-
 template <int W, int C, int OUT, int SPS>
 __device__ __forceinline__ void conv3x3i_init(const ConvArgs& a, int8_t* lds) {
   using G = IGeo<W, SPS>;
@@ -286,20 +289,26 @@ struct WideStream {
 
 // RELU (int8, OUT == 0): the output clamp is [0, 127] and the requantisation
 // takes the v_cvt_pk_u8_f32 form (device_common.h quant4_relu).
-// DSR (int8, RES, RELU): a downsampling block's conv2, whose residual is the
-// block's 1x1/s2 downsample (infer_e2e.cu:187-199) computed here instead of
-// read: per tile KD = C/64 v_mfma_i32_32x32x32_i8 on A fragments of the
-// downsample weights (the wave's 32 channels, loaded once per item) and B
-// fragments of the block input at (2 oh, 2 ow) (16 bytes per lane and k-step,
-// loaded one tile ahead), requantised exactly as the downsample's own epilogue
-// (device_common.h epi4_dsr_relu).  int32 sums are order-free, so the
-// residual is bit-identical to the fused stride-2 kernel's downsample output;
-// that kernel then runs conv1 alone.
-template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false, bool RELU = false, bool DSR = false>
+// DSR (int8, RES, RELU; 28x28 and 14x14): a downsampling block's conv2, whose
+// residual is the block's 1x1/s2 downsample (infer_e2e.cu:187-199) computed
+// here instead of read: in each item's second-to-last stage the item's block
+// input pixels at (2 oh, 2 ow) (C/2 bytes each, 16-byte chunks XOR-swizzled
+// by pixel) and the downsample's alpha / beta of the item's 128 channels come
+// in by LDS-DMA beside the ring (the last stage's barrier publishes them); the
+// last stage's start loads the wave's downsample weights (A fragments, C/64
+// k-steps) into registers; the epilogue runs per tile the C/64 MFMAs on B
+// fragments read from LDS (the next tile's while this tile requantises) and
+// requantises downsample and conv together (device_common.h epi4_dsr_relu:
+// bit-identical to the downsample's own int8 output added as the residual).
+// The stride-2 conv1 of the block then runs without its fused downsample.
+template <int W, int C, int OUT, bool RES, int NF, int NLD, bool F8 = false, bool RELU = false, bool DSR = false,
+          bool GAP = false>
 __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, int wave, int mt, int f0) {
-  static_assert(!DSR || (OUT == 0 && RES && RELU && !F8), "the downsample residual is an int8 ReLU epilogue");
-  constexpr bool RESL = RES;  // the residual is loaded (DSR: from y, where the item's downsample was stored)
+  static_assert(!GAP || (W == 7 && C == 512 && OUT == 0 && !F8), "the pooled head follows the 7x7x512 conv");
+  static_assert(!DSR || (OUT == 0 && RES && RELU && !F8 && W != 7), "the downsample residual: int8 ReLU, 28x28 / 14x14");
+  constexpr bool RESL = RES && !DSR;  // the residual is loaded (DSR: computed)
   constexpr int KD = C / 64;          // DSR: downsample k-steps (the block input has C/2 channels)
+  using DG = DsrGeo<W, C>;
   constexpr int SPS = sps_of<W, F8>();
   using G = IGeo<W, SPS>;
   constexpr int NS = C / ISC / SPS;  // stages (SPS 32-channel slices each)
@@ -349,113 +358,11 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   Acc acc[NF];
   v4i rq[NF];
   int cur_ot = 0, cur_p0 = 0;
-  // DSR: the item's downsample, computed before its first stage's MFMAs
-  // (ds_issue + ds_compute): A fragments of the downsample weights (this
-  // wave's 32 channels; k-step kk = block-input channels 32 kk + 16 lh ..),
-  // its alpha / beta, and B fragments of each tile's pixels at (2 oh, 2 ow)
-  // of the block input through a ring of RB tiles; the int8 results stay in
-  // rds[f] (MFMA layout: byte e of rds[f][g] = channel 8 g + 4 lh + e) until
-  // the item's epilogue adds them as the residual.
-  constexpr int KDA = DSR ? KD : 1;
-  constexpr int RB = !DSR ? 1 : KD <= 2 ? NF : KD == 4 ? 3 : 2;
-  v4i ads[KDA], dab[DSR ? 8 : 1], bq[RB][KDA];
-  int ds_ot = 0, ds_p0 = 0;
-  auto ds_bload = [&](int f, v4i(&b)[KDA]) {
-    const int lp = (f0 + f) * 32 + lr, p = ds_p0 + lp;
-    const int pp = lp < IL && p < a.P ? p : 0;
-    const int n = pp / (W * W), r = pp - n * (W * W), oh = r / W, ow = r - oh * W;
-    const int8_t* src = a.ds_x + (size_t)((n * 2 * W + 2 * oh) * 2 * W + 2 * ow) * (C / 2) + lh * 16;
-#pragma unroll
-    for (int kk = 0; kk < KDA; ++kk) b[kk] = gload16_untracked(src + kk * 32);
-  };
-  auto ds_issue = [&](int li) {  // the item's loads: A fragments, alpha / beta, the first RB tiles
-    if constexpr (!DSR) return;
-    item_of(li, ds_ot, ds_p0);
-    const int o = ds_ot * G::OT + mt * 32 + lr;
-#pragma unroll
-    for (int kk = 0; kk < KDA; ++kk)
-      ads[kk] = gload16_untracked(a.ds_w + ((size_t)((o >> 7) * KD + kk) * 128 + (o & 127)) * 48 + lh * 16);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int oc = ds_ot * G::OT + mt * 32 + 8 * g + 4 * lh;
-      dab[2 * g] = gload16_untracked(a.ds_alpha + oc);
-      dab[2 * g + 1] = gload16_untracked(a.ds_beta + oc);
-    }
-#pragma unroll
-    for (int f = 0; f < RB; ++f) ds_bload(f, bq[f]);
-  };
-  // FIRST: the first item's stage-0 LDS-DMA was issued between ds_issue and
-  // ds_compute, so it is younger than the first RB tiles' loads; the waits
-  // count it as the fewest unmasked pieces any wave issues (a lower bound on
-  // what vmcnt counts: safe whether masked pieces count or not)
-  auto ds_compute = [&](auto first_c) {
-    if constexpr (DSR) {
-      constexpr int NDMA = decltype(first_c)::value ? G::PPS / NLD + G::WPS / NLD : 0;
-      // tile f's downsample requantised as its own epilogue would (conv3x3s2i
-      // DS: signed clamp) and stored, in the store layout, where the item's
-      // output goes: the epilogue reads it back as the residual (this wave's
-      // own bytes, an L2 hit) and overwrites it
-      auto requant = [&](const v16i& ac, int f) {
-        unsigned q[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float al4[4] = {__int_as_float(dab[2 * g][0]), __int_as_float(dab[2 * g][1]),
-                                __int_as_float(dab[2 * g][2]), __int_as_float(dab[2 * g][3])};
-          const float be4[4] = {__int_as_float(dab[2 * g + 1][0]), __int_as_float(dab[2 * g + 1][1]),
-                                __int_as_float(dab[2 * g + 1][2]), __int_as_float(dab[2 * g + 1][3])};
-          const int a4[4] = {ac[4 * g], ac[4 * g + 1], ac[4 * g + 2], ac[4 * g + 3]};
-          q[g] = epi4(a4, al4, be4, -127.f);
-        }
-        swap32(q[0], q[2]);
-        swap32(q[1], q[3]);
-        const int lp = (f0 + f) * 32 + lr, p = ds_p0 + lp;
-        const bool keep = lp < IL && p < a.P;
-        v4i* dst = keep ? (v4i*)((int8_t*)a.y + (size_t)p * a.OC + ds_ot * G::OT + mt * 32 + lh * 16)
-                        : (v4i*)(g_trash_i + lane * 16);
-        *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
-      };
-      v16i prev = v16i{0};
-      auto tile = [&](auto fc) {
-        constexpr int f = decltype(fc)::value;
-        // younger than tile f's loads: the later tiles issued so far (and the DMA)
-        constexpr int CNT = ((f + RB - 1 < NF - 1 ? f + RB - 1 : NF - 1) - f) * KDA + (f < RB ? NDMA : 0);
-        v4i(&b)[KDA] = bq[f % RB];
-        wait_vm_tie_frags<CNT>(b);
-        if constexpr (f == 0) {
-          tie_frags(ads);
-          tie_frags(dab);
-        }
-        v16i accd = v16i{0};
-#pragma unroll
-        for (int kk = 0; kk < KDA; ++kk) accd = __builtin_amdgcn_mfma_i32_32x32x32_i8(ads[kk], b[kk], accd, 0, 0, 0);
-        if constexpr (f > 0) requant(prev, f - 1);
-        if constexpr (f + RB < NF) ds_bload(f + RB, b);
-        prev = accd;
-      };
-      static_for_i<0, NF>(tile);
-      requant(prev, NF - 1);
-    }
-  };
-
   ISTAMP(0);
-  // DSR: the first item's downsample loads go out ahead of stage 0's DMA, and
-  // its MFMAs and requantisation run while that DMA lands (the launch's cold
-  // prologue)
-  if constexpr (DSR) ds_issue(0);
   if (loader) {
     prep_for(0);
 #pragma unroll
     for (int k = 0; k < DPW; ++k) issue_piece(0, k);
-  }
-  if constexpr (DSR) {
-    ds_compute(std::true_type{});
-    // the workgroup's later items (two per CU in the 28x28 launch): stored
-    // the same way now, not between items -- a downsample phase inside the
-    // stage loop made the compiler spill the k-loop's registers
-    for (int li = 1; li < st.nst / NS; ++li) {
-      ds_issue(li);
-      ds_compute(std::false_type{});
-    }
   }
   if (DLQ_ABL(a, 256)) {  // probe builds: stage 0 landed from a cold L2, then the same pieces again (L2-hot)
     wait_vm_const<0>();
@@ -493,6 +400,40 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       item_of(li, cur_ot, cur_p0);
 #pragma unroll
       for (int f = 0; f < NF; ++f) acc[f] = Acc{0};
+    }
+    v4i ads[DSR ? KD : 1];  // DSR: the downsample weights' A fragments (the item's last stage)
+    constexpr bool DS_EARLY = KD <= 2;
+    auto ds_aload = [&]() {
+      const int o = cur_ot * G::OT + mt * 32 + lr;
+#pragma unroll
+      for (int kk = 0; kk < (DSR ? KD : 1); ++kk)
+        ads[kk] = gload16_untracked(a.ds_w + ((size_t)((o >> 7) * KD + kk) * 128 + (o & 127)) * 48 + lh * 16);
+    };
+    if constexpr (DSR) {
+      if (j == NS - 2) {
+        // the item's block-input pixels and downsample alpha / beta (piece
+        // NPD: lanes 0-31 alpha, 32-63 beta of the item's 128 channels)
+        for (int pc = wave; pc <= DG::NPD; pc += INW) {
+          const int8_t* src;
+          unsigned dst;
+          if (pc < DG::NPD) {
+            const int u = pc * 64 + lane, lp = u / DG::NCH, c = (u - lp * DG::NCH) ^ DG::swz(lp), p = cur_p0 + lp;
+            const int n = p / (W * W), r = p - n * (W * W), oh = r / W, ow = r - oh * W;
+            src = lp < IL && p < a.P ? a.ds_x + (size_t)((n * 2 * W + 2 * oh) * 2 * W + 2 * ow) * (C / 2) + c * 16
+                                     : g_zero_i + (lane & 3) * 16;
+            dst = lds_addr32(lds) + DG::OFF_DS + pc * 1024;
+          } else {
+            const int o = cur_ot * G::OT + (lane & 31) * 4;
+            src = (const int8_t*)((lane < 32 ? a.ds_alpha : a.ds_beta) + o);
+            dst = lds_addr32(lds) + DG::OFF_DAB;
+          }
+          glds16_asm(src, dst);
+        }
+      }
+      // the A fragments: ahead of the last stage's DMA (awaited in the
+      // epilogue by a count of it) where the k-loop has the registers; the
+      // 14x14 launch's four (16 VGPRs) wait for the epilogue (they spilled)
+      if (j == NS - 1 && DS_EARLY) ds_aload();
     }
     const bool dma = more && loader && !DLQ_ABL(a, 2);  // compile-time true in library builds
     const int sb = (s & 1) * G::SLOT;
@@ -563,7 +504,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       const int p = cur_p0 + (f0 + f) * 32 + lr;
       const bool keep = (f0 + f) * 32 + lr < IL && p < a.P;
       const size_t off = keep ? (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16 : 0;
-      rq[f] = gload16_untracked((DSR ? (const int8_t*)a.y : a.res) + off);
+      rq[f] = gload16_untracked(a.res + off);
     };
     if constexpr (PF2) {
     // B fragments two k-steps ahead: fb[ks & 1][f] holds k-step ks of tile f
@@ -664,6 +605,17 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 
     ISTAMP(2 + 2 * s);
     if (j != NS - 1 || DLQ_ABL(a, 4)) return;  // probe builds: timing without the epilogue
+    // GAP: the item's outputs are also staged in LDS for the pooling: in the
+    // launch's last stage in the idle slot (past the prefetch pieces' first
+    // KiB), no wait; in an earlier item's last stage the idle slot is
+    // receiving the next item's stage 0, so this stage's slot is used, once
+    // every wave is past its last fragment read (a barrier: the epilogues
+    // then no longer overlap the slower waves' MFMAs)
+    constexpr bool LAST_STAGE = !decltype(more_c)::value;
+    const int gstage = LAST_STAGE ? (((s + 1) & 1) * G::SLOT + 1024) : sb;
+    if constexpr (GAP && !LAST_STAGE) __builtin_amdgcn_s_barrier();
+    static_assert(!GAP || 1024 + IL * 64 <= G::SLOT, "the pooling stage fits a slot");
+    (void)gstage;
     // ---- fused epilogue of the item ----
     if constexpr (OUT == 2) {
 #pragma unroll
@@ -680,6 +632,61 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
           else
             *dst = v4i{acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
         }
+      }
+    } else if constexpr (DSR) {
+      // the A fragments, issued before this stage's DMA: younger than them
+      // at most the fewest unmasked pieces any wave issued (a lower bound on
+      // what vmcnt counts), none in the launch's last stage
+      constexpr int YOUNG = decltype(more_c)::value && DS_EARLY ? G::PPS / NLD + G::WPS / NLD : 0;
+      if constexpr (!DS_EARLY) ds_aload();
+      wait_vm_tie_frags<YOUNG>(ads);
+      // tile f's downsample accumulators (B fragments from the pixel region)
+      auto ds_acc = [&](int f) {
+        int lp = (f0 + f) * 32 + lr;
+        lp = lp < IL ? lp : IL - 1;
+        const int8_t* base = lds + DG::OFF_DS + lp * DG::NCH * 16;
+        v16i ad = v16i{0};
+#pragma unroll
+        for (int kk = 0; kk < KD; ++kk)
+          ad = __builtin_amdgcn_mfma_i32_32x32x32_i8(ads[kk], *(const v4i*)(base + (((2 * kk + lh) ^ DG::swz(lp)) << 4)),
+                                                     ad, 0, 0, 0);
+        return ad;
+      };
+      // 28x28: the next tile's MFMAs run beside this tile's requantisation;
+      // 14x14 (four MFMAs per tile): one tile at a time (a second set spilled)
+      constexpr bool PIPE = KD <= 2;
+      v16i adn = PIPE ? ds_acc(0) : v16i{0};
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        // one tile per scheduling region: hoisting later tiles' fragment
+        // reads above this one spilled the epilogue's registers
+        __builtin_amdgcn_sched_barrier(0);
+        const v16i ad = PIPE ? adn : ds_acc(f);
+        if (PIPE && f + 1 < NF) adn = ds_acc(f + 1);
+        unsigned q[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          // alpha / beta of conv and downsample for this group's 4 channels,
+          // from LDS per tile (registers are what this epilogue is short of)
+          const int ol = mt * 32 + 8 * g + 4 * lh, oc = cur_ot * G::OT + ol;
+          const v4i v[4] = {*(const v4i*)(lds + OFF_AB + oc * 4), *(const v4i*)(lds + OFF_AB + (C + oc) * 4),
+                            *(const v4i*)(lds + DG::OFF_DAB + ol * 4), *(const v4i*)(lds + DG::OFF_DAB + 512 + ol * 4)};
+          float ab[4][4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ab[t][e] = __int_as_float(v[t][e]);
+          const int ac[4] = {acc[f][4 * g], acc[f][4 * g + 1], acc[f][4 * g + 2], acc[f][4 * g + 3]};
+          const int adc[4] = {ad[4 * g], ad[4 * g + 1], ad[4 * g + 2], ad[4 * g + 3]};
+          q[g] = epi4_dsr_relu(ac, ab[0], ab[1], adc, ab[2], ab[3], a.s_res);
+        }
+        swap32(q[0], q[2]);
+        swap32(q[1], q[3]);
+        const int lp = (f0 + f) * 32 + lr, p = cur_p0 + lp;
+        const bool keep = lp < IL && p < a.P;
+        v4i* dst = keep ? (v4i*)((int8_t*)a.y + (size_t)p * a.OC + cur_ot * G::OT + mt * 32 + lh * 16)
+                        : (v4i*)(g_trash_i + lane * 16);
+        *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
       }
     } else {
       const float lo = a.relu ? 0.f : (F8 ? -448.f : -127.f);
@@ -743,6 +750,56 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
                                           ((size_t)a.P * a.OC) + lane * 16);
         if (!DLQ_ABL(a, 64))  // probe builds: dbg 64 drops the int8 stores
           *dst = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
+        if constexpr (GAP) {  // [392 px][64 ch] staging, 16-byte chunk c at c ^ (px & 3)
+          if (lp < IL)
+            *(v4i*)(lds + gstage + lp * 64 + 16 * ((2 * mt + lh) ^ (lp & 3))) = v4i{(int)q[0], (int)q[2], (int)q[1], (int)q[3]};
+        }
+      }
+      if constexpr (GAP) {
+        // The item's 8 whole images x 64 channels, pooled from the staged
+        // bytes by all 8 waves: thread = (image, 8 channels, pixel group of
+        // 8); the ReLU outputs are 0..127, so two channels add in the two
+        // 16-bit halves of one int32 (49 x 127 < 2^16) -- exact integer sums
+        // as gap16_kernel's; the 8 pixel groups of a row of lanes reduce by
+        // three DPP row shifts into its lane 7, which requantises (sat_rne,
+        // as gap16_kernel) and stores the 8 codes the FC reads
+        // (infer_e2e.cu:417-425).
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes
+        __builtin_amdgcn_s_barrier();
+        {
+          const int t = threadIdx.x, nl = t >> 6, cg8 = (t >> 3) & 7, pg = t & 7;
+          const int n = cur_p0 / 49 + nl;
+          unsigned sm[4] = {0u, 0u, 0u, 0u};  // channels {0,2} {1,3} {4,6} {5,7} of the group
+#pragma unroll
+          for (int jj = 0; jj < 7; ++jj) {
+            const int i = pg + 8 * jj, px = nl * 49 + i;
+            if (i < 49) {
+              const v2i v = *(const v2i*)(lds + gstage + px * 64 + 16 * ((cg8 >> 1) ^ (px & 3)) + 8 * (cg8 & 1));
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                sm[2 * h] += (unsigned)v[h] & 0x00ff00ffu;
+                sm[2 * h + 1] += ((unsigned)v[h] >> 8) & 0x00ff00ffu;
+              }
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {  // row_shr 1, 2, 4 (out-of-row lanes read 0): lane 7 of each 8 = the sum
+            sm[i] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)sm[i], 0x111, 0xf, 0xf, true);
+            sm[i] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)sm[i], 0x112, 0xf, 0xf, true);
+            sm[i] += (unsigned)__builtin_amdgcn_update_dpp(0, (int)sm[i], 0x114, 0xf, 0xf, true);
+          }
+          if (n < a.N && pg == 7) {
+            unsigned o[2] = {0u, 0u};
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int b = 0; b < 4; ++b) {  // channel 4h + b: half b >> 1 of sm[2h + (b & 1)]
+                const unsigned v = (sm[2 * h + (b & 1)] >> (16 * (b >> 1))) & 0xffffu;
+                o[h] |= ((unsigned)sat_rne((float)(int)v * a.gap_k) & 0xffu) << (8 * b);
+              }
+            *(v2i*)(a.gap_y + (size_t)n * C + cur_ot * G::OT + cg8 * 8) = v2i{(int)o[0], (int)o[1]};
+          }
+        }
       }
     }
     };
@@ -757,11 +814,11 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   ISTAMP(63);
 }
 
-template <int W, int C, int OUT, bool RES, bool F8 = false, bool RELU = false, bool DSR = false>
+template <int W, int C, int OUT, bool RES, bool F8 = false, bool RELU = false, bool DSR = false, bool GAP = false>
 __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   using G = IGeo<W, sps_of<W, F8>()>;
   constexpr int OFF_AB = G::OFF_AB;
-  constexpr int LDS_TOTAL = OFF_AB + 2 * C * 4;
+  constexpr int LDS_TOTAL = DSR ? DsrGeo<W, C>::LDS_END : OFF_AB + 2 * C * 4;
   static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
   const int tid = threadIdx.x;
@@ -772,14 +829,14 @@ __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   // for every wave, WideStream): two bodies per kernel
   if constexpr (G::MT == 4) {
     if (wave < 4)
-      conv3x3i_body<W, C, OUT, RES, 7, INW, F8, RELU, DSR>(a, lds, wave, mt, f0);
+      conv3x3i_body<W, C, OUT, RES, 7, INW, F8, RELU, DSR, GAP>(a, lds, wave, mt, f0);
     else
-      conv3x3i_body<W, C, OUT, RES, 6, INW, F8, RELU, DSR>(a, lds, wave, mt, f0);
+      conv3x3i_body<W, C, OUT, RES, 6, INW, F8, RELU, DSR, GAP>(a, lds, wave, mt, f0);
   } else {
     if (wave < 2)
-      conv3x3i_body<W, C, OUT, RES, 4, INW, F8, RELU, DSR>(a, lds, wave, mt, f0);
+      conv3x3i_body<W, C, OUT, RES, 4, INW, F8, RELU, DSR, GAP>(a, lds, wave, mt, f0);
     else
-      conv3x3i_body<W, C, OUT, RES, 3, INW, F8, RELU, DSR>(a, lds, wave, mt, f0);
+      conv3x3i_body<W, C, OUT, RES, 3, INW, F8, RELU, DSR, GAP>(a, lds, wave, mt, f0);
   }
   (void)nf;
 }
@@ -835,9 +892,8 @@ hipError_t launch_conv3x3i_dsr(const ConvArgs& a, hipStream_t s) {
   switch (a.W) {
     case 28: return a.C == 128 ? launch_ci_dsr<28, 128>(a, s) : hipErrorInvalidValue;
     case 14: return a.C == 256 ? launch_ci_dsr<14, 256>(a, s) : hipErrorInvalidValue;
-    case 7: return a.C == 512 ? launch_ci_dsr<7, 512>(a, s) : hipErrorInvalidValue;
   }
-  return hipErrorInvalidValue;
+  return hipErrorInvalidValue;  // 7x7x512: the LDS holds no pixel region beside its two-slice ring
 }
 
 // e4m3 operands, same shapes and weight image layout (conv3x3w_pack of the codes).
@@ -854,6 +910,15 @@ hipError_t launch_conv3x3i_f8(const ConvArgs& a, hipStream_t s) {
 // Weight image: conv3x3w_pack (wpack.cpp).
 hipError_t launch_conv3x3i(const ConvArgs& a, hipStream_t s) {
   if (a.ds_x) return launch_conv3x3i_dsr(a, s);
+  if (a.gap_y) {  // the pooled head after the last conv: 7x7x512, int8, ReLU, residual
+    if (a.OCp != a.OC || a.C != 512 || a.OC != 512 || a.H != 7 || a.W != 7 || a.out_kind != 0 || !a.relu || !a.res)
+      return hipErrorInvalidValue;
+    using G = IGeo<7, sps_of<7, false>()>;
+    const int NI = (a.OCp / G::OT) * ((a.P + IL - 1) / IL), ncu = num_cus_i();
+    hipLaunchKernelGGL((conv3x3i_kernel<7, 512, 0, true, false, true, false, true>), dim3(NI < ncu ? NI : ncu),
+                       dim3(INW * 64), 0, s, a);
+    return hipGetLastError();
+  }
   if (a.OCp != a.OC || a.C != a.OC || a.H != a.W) return hipErrorInvalidValue;
   switch (a.W) {
     case 28: return a.C == 128 ? launch_ci<28, 128>(a, s) : hipErrorInvalidValue;

@@ -12,7 +12,7 @@ namespace dlq {
 // Host-side knobs behind dlq_set_knob (capi.cpp): initialised once from the
 // environment when the library loads, never read from it on the hot path.
 extern std::atomic<int> g_knob_l1_grid, g_knob_head_split, g_knob_graph, g_knob_gemm_tile, g_knob_ds_split,
-    g_knob_prefetch;
+    g_knob_prefetch, g_knob_gap_epi;
 extern std::atomic<unsigned> g_knob_gen;
 
 
@@ -50,6 +50,11 @@ struct ConvArgs {
   const float* ds_beta;
   int ds_C;
   Prefetch pf;  // the next launch's first weight blocks (engine forwards only)
+  // The network's last conv (layer4.1 conv2, 7x7x512): its int8 output's
+  // global average pool computed per item right after the item's epilogue
+  // (conv3x3i.hip GAP): gap_y[N][512] int8 = clamp(rne(float(sum) * gap_k)).
+  int8_t* gap_y;
+  float gap_k;
 };
 
 // Timing-ablation switches exist only in probe builds (tools/probe/*.hip
@@ -193,9 +198,11 @@ int conv_args_checked(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_p
                       ConvArgs& a);
 // dlq_conv2d_nhwc_s8 / dlq_conv2d_s2_ds_nhwc_s8 with the next launch's weight
 // regions (Prefetch; nullptr = none) for the engine's forward.
+// gap_y: the wide 7x7x512 conv also writes its output's int8 GAP codes
+// (ConvArgs::gap_y / gap_k; the network's last conv only).
 int conv2d_nhwc_s8_pf(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
                       const float* beta, const int8_t* residual, float res_scale, int relu, int out_kind, void* y,
-                      void* stream, const Prefetch* pf);
+                      void* stream, const Prefetch* pf, int8_t* gap_y = nullptr, float gap_k = 0.f);
 int conv2d_s2_ds_nhwc_s8_pf(const dlq_conv_desc* d, const int8_t* x, const int8_t* w_packed, const float* alpha,
                             const float* beta, const int8_t* w_ds, const float* alpha_ds, const float* beta_ds,
                             int8_t* y, int8_t* y_ds, void* stream, const Prefetch* pf);

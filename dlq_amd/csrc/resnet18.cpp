@@ -223,29 +223,36 @@ float inv_scale(float s) { return 1.0f / s; }
 // launches (gap16_kernel + linear_kernel) instead of the fused gap_fc_kernel.
 bool head_split() { return g_knob_head_split.load(std::memory_order_relaxed) == 1; }
 
-// Knob "ds_split" (DLQ_DS_SPLIT=1, dlq_set_knob): a downsampling block's
-// 1x1/s2 downsample computed by its conv2 launch (conv3x3i DSR, stored where
-// conv2's output goes and read back as the residual) instead of fused into
-// the stride-2 conv1 launch (conv3x3s2i DS, the default).
-bool ds_split() { return g_knob_ds_split.load(std::memory_order_relaxed) == 1; }
+// Knob "ds_split" (DLQ_DS_SPLIT): 0 = default on, -1 = off.  A downsampling
+// block's 1x1/s2 downsample is computed by its conv2 launch (conv3x3i DSR;
+// layer2.0 and layer3.0) and its stride-2 conv1 runs alone, instead of the
+// downsample fused into the stride-2 launch (conv3x3s2i DS, stored and read
+// back as conv2's residual; layer4.0 always, or every block with -1).
+bool ds_split() { return g_knob_ds_split.load(std::memory_order_relaxed) >= 0; }
 
 // Knob "prefetch" (DLQ_PREFETCH): 0 = default on, -1 = off.  Each wide /
 // stride-2 conv launch's last stage reads the next launch's first weight
 // stages (Prefetch, device_common.h prefetch_next).
 bool prefetch_on() { return g_knob_prefetch.load(std::memory_order_relaxed) >= 0; }
 
+// Knob "gap_epi" (DLQ_GAP_EPI): 0 = default on, -1 = off.  The last conv
+// (layer4.1 conv2) pools its own output (conv3x3i GAP) and the head is the
+// FC alone (linear512_f32_kernel), instead of the fused gap_fc_kernel.
+bool gap_epi_on() { return g_knob_gap_epi.load(std::memory_order_relaxed) >= 0; }
+
 // conv2d_nchw_im2col_gemm + bn_launch (+ add_inplace + relu_forward) of the
 // reference, as one implicit-GEMM launch with the epilogue fused.
 int conv2d_nhwc_s8(const dlq_resnet18* m, const ConvLayer& c, const int8_t* x, int N, int H, int W,
                    const int8_t* residual, float res_scale, bool relu, int8_t* y, hipStream_t s,
-                   int* OH, int* OW, const Prefetch* pf = nullptr) {
+                   int* OH, int* OW, const Prefetch* pf = nullptr, int8_t* gap_y = nullptr, float gap_k = 0.f) {
   dlq_conv_desc d{N, H, W, c.Cstore, c.OC, c.k, c.k, c.s, c.s, c.p, c.p};
   *OH = out_dim(H, c.k, c.s, c.p);
   *OW = out_dim(W, c.k, c.s, c.p);
   // alpha/beta are already in this conv's output-grid units (prepare); the
   // residual's scale is converted the same way.
   const float r_s = residual ? dlq::res_scale(res_scale, m->scales.at(c.site)) : 0.f;
-  return conv2d_nhwc_s8_pf(&d, x, c.w, c.alpha, c.beta, residual, r_s, relu ? 1 : 0, DLQ_OUT_S8, y, s, pf);
+  return conv2d_nhwc_s8_pf(&d, x, c.w, c.alpha, c.beta, residual, r_s, relu ? 1 : 0, DLQ_OUT_S8, y, s, pf, gap_y,
+                           gap_k);
 }
 
 // The first weight stages a launch of conv `c` (input H x H) streams: the
@@ -322,7 +329,7 @@ Prefetch block_prefetch(const dlq_resnet18* m, const Block& b, int H) {
 // identity | 1x1 downsample-bn, add, relu -- three launches at most.
 int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N, int H,
                         int W, int8_t* h, int8_t* dsb, int8_t* out, hipStream_t s, int* OH,
-                        int* OW, const Prefetch* next = nullptr) {
+                        int* OW, const Prefetch* next = nullptr, int8_t* gap_y = nullptr, float gap_k = 0.f) {
   int h1, w1, h2, w2;
   const ConvLayer& c1 = m->convs[b.c1];
   const int8_t* skip = in;
@@ -344,7 +351,7 @@ int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N
   const ConvLayer* c2w = &m->convs[b.c2];
   if (b.down && m->convs[b.ds].wf && ds_split() && conv3x3s2_shape(c1.Cstore, c1.OC, H, W, 3, 3, 2, 2, 1, 1) &&
       wide_layout(c1.Cstore, c1.OC, H, W, 3, 3, 2, 2, 1, 1) &&
-      conv3x3w_shape(c2w->Cstore, c2w->OC, H / 2, W / 2, 3, 3, 1, 1, 1, 1) && c2w->Cstore == c1.OC &&
+      conv3x3w_shape(c2w->Cstore, c2w->OC, H / 2, W / 2, 3, 3, 1, 1, 1, 1) && H / 2 != 7 && c2w->Cstore == c1.OC &&
       m->convs[b.ds].OC == c1.OC && 2 * c1.Cstore == c1.OC) {
     // conv1 (3x3/s2) alone, then conv2 with the 1x1/s2 downsample computed
     // and requantised in its epilogue as the residual (conv3x3i DSR): the
@@ -353,10 +360,12 @@ int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N
     const ConvLayer& c2 = *c2w;
     dlq_conv_desc d{N, H, W, c1.Cstore, c1.OC, 3, 3, 2, 2, 1, 1};
     if ((rc = mark(m, s, DLQ_FAM_S2DS))) return rc;
-    rc = dlq_conv2d_nhwc_s8(&d, in, c1.w, c1.alpha, c1.beta, nullptr, 0.f, 1, DLQ_OUT_S8, h, s);
-    if (rc) return rc;
     h1 = out_dim(H, 3, 2, 1);
     w1 = out_dim(W, 3, 2, 1);
+    const Prefetch pf2 = conv_prefetch(c2, h1);
+    rc = conv2d_nhwc_s8_pf(&d, in, c1.w, c1.alpha, c1.beta, nullptr, 0.f, 1, DLQ_OUT_S8, h, s,
+                           prefetch_on() ? &pf2 : nullptr);
+    if (rc) return rc;
     if ((rc = mark(m, s, conv_family(c2, h1)))) return rc;
     dlq_conv_desc d2{N, h1, w1, c2.Cstore, c2.OC, 3, 3, 1, 1, 1, 1};
     ConvArgs a;
@@ -367,6 +376,7 @@ int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N
     a.ds_alpha = ds.alpha;
     a.ds_beta = ds.beta;
     a.ds_C = c1.Cstore;
+    if (next && prefetch_on()) a.pf = *next;
     if (a.P) {
       hipError_t e = launch_conv3x3i_dsr(a, s);
       if (e != hipSuccess) return hip_fail(e, "conv2 + downsample residual launch");
@@ -407,7 +417,7 @@ int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N
   }
   if ((rc = mark(m, s, conv_family(m->convs[b.c2], h1)))) return rc;
   rc = conv2d_nhwc_s8(m, m->convs[b.c2], h, N, h1, w1, skip, s_skip, true, out, s, &h2, &w2,
-                      prefetch_on() ? next : nullptr);
+                      prefetch_on() ? next : nullptr, gap_y, gap_k);
   *OH = h2;
   *OW = w2;
   return rc;
@@ -1011,6 +1021,7 @@ int forward_pass(dlq_resnet18* m, const float* x, int B, float* logits, hipStrea
   }
   if (record && (rc = record_stage(m, "stem_pool", cur, nB * H * W * 64, s))) return rc;
   // 2-5) layer1..layer4 (:300-415)
+  bool pooled = false;  // the last conv wrote the GAP codes (gap_epi)
   for (size_t bi = 0; bi < m->blocks.size(); ++bi) {
     const Block& b = m->blocks[bi];
     int fi[3];
@@ -1029,8 +1040,21 @@ int forward_pass(dlq_resnet18* m, const float* x, int B, float* logits, hipStrea
       next.stride[0] = 0;
       next.len[0] = (int)(packed_bytes(1000, 512, 1, 1) & ~(size_t)1023);
     }
-    rc = basic_block_forward(m, b, cur, B, H, W, bufp(fi[0]), bufp(fi[1]), bufp(fi[2]), s, &OH, &OW, &next);
+    // the last block's conv2 pools its own output (its H is the block's input
+    // H: layer4.1 keeps the resolution) when it is the wide 7x7x512 conv
+    int8_t* gap_y = nullptr;
+    float gap_k = 0.f;
+    if (bi + 1 == m->blocks.size() && gap_epi_on() && !head_split() && b.stride == 1 && !b.down) {
+      const ConvLayer& c2 = m->convs[b.c2];
+      if (H == 7 && W == 7 && c2.Cstore == 512 && c2.OC == 512 && conv3x3w_shape(512, 512, 7, 7, 3, 3, 1, 1, 1, 1)) {
+        gap_y = gq;
+        gap_k = (m->scales.at(c2.site) / (float)(H * W)) / m->scales.at("gap");
+      }
+    }
+    rc = basic_block_forward(m, b, cur, B, H, W, bufp(fi[0]), bufp(fi[1]), bufp(fi[2]), s, &OH, &OW, &next, gap_y,
+                             gap_k);
     if (rc) return rc;
+    pooled = gap_y != nullptr;
     ci = fi[2];
     cur = bufp(ci);
     H = OH;
@@ -1041,6 +1065,13 @@ int forward_pass(dlq_resnet18* m, const float* x, int B, float* logits, hipStrea
   // 6) GAP + FC (:417-433)
   const std::string last = m->convs[m->blocks.back().c2].site;
   const float k = (m->scales.at(last) / (float)(H * W)) / m->scales.at("gap");
+  if (pooled) {  // the last conv wrote the GAP codes: the FC alone
+    if (record) m->stage["gap"] = {gq, nB * 512};
+    if ((rc = mark(m, s, DLQ_FAM_FC))) return rc;
+    rc = dlq_linear_s8(gq, B, 512, m->fc_w, 1000, m->fc_alpha, m->fc_beta, 0, DLQ_OUT_F32, logits, stream);
+    if (rc) return rc;
+    return mark(m, s, -1);
+  }
   if ((rc = mark(m, s, DLQ_FAM_GAP))) return rc;
   if (!m->keep && !head_split()) {  // one launch (head.hip gap_fc_kernel); the GAP codes stay on chip
     rc = dlq_gap_fc_s8(cur, B, 512, H * W, k, m->fc_w, 1000, m->fc_alpha, m->fc_beta, logits, stream);

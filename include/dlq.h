@@ -117,11 +117,17 @@ int dlq_pack_conv_weights_s8(const dlq_conv_desc* d, const int8_t* q_oihw, int I
  *   "graph"      (DLQ_GRAPH)      1 = replay the forward as a hipGraph;
  *   "gemm_tile"  (DLQ_GEMM_TILE)  dlq_gemm_s8s8s32's tile, 0 = by shape,
  *                                 1 = 256 x 256, 2 = 256 x 128, 3 = 128 x 128;
- *   "ds_split"   (DLQ_DS_SPLIT)   1 = the engine computes a downsampling
- *                                 block's 1x1/s2 downsample in its conv2
- *                                 launch (dlq_conv2d_dsres_nhwc_s8) instead of
- *                                 fusing it into the stride-2 conv1 launch
- *                                 (dlq_conv2d_s2_ds_nhwc_s8, the default).
+ *   "ds_split"   (DLQ_DS_SPLIT)   0 = (default) the engine computes the
+ *                                 layer2.0 / layer3.0 1x1/s2 downsample in
+ *                                 their conv2 launch (dlq_conv2d_dsres_nhwc_s8);
+ *                                 -1 = fused into the stride-2 conv1 launch
+ *                                 (dlq_conv2d_s2_ds_nhwc_s8) as for layer4.0;
+ *   "prefetch"   (DLQ_PREFETCH)   0 = (default) each launch of a forward
+ *                                 reads the next launch's first weights during
+ *                                 its last stage; -1 = off;
+ *   "gap_epi"    (DLQ_GAP_EPI)    0 = (default) the last conv pools its own
+ *                                 output and the head is the FC alone;
+ *                                 -1 = the fused GAP + FC head launch.
  * Returns DLQ_ERR_ARG for an unknown name. */
 int dlq_set_knob(const char* name, int value);
 int dlq_get_knob(const char* name, int* value);
@@ -224,8 +230,8 @@ int dlq_conv2d_s2_ds_nhwc_s8(const dlq_conv_desc* d, const int8_t* x, const int8
 
 /* Downsampling BasicBlock back (infer_e2e.cu:177-186 conv2 + bn, :187-196
  * the 1x1/s2 downsample conv + bn, :197-202 add + relu) in one launch: the
- * 3x3/s1/p1 conv of h (d: C == OC, the layer2-4 shapes 28x28x128, 14x14x256,
- * 7x7x512; w_packed from dlq_pack_conv_weights_s8) -> alpha/beta, plus the
+ * 3x3/s1/p1 conv of h (d: C == OC, the layer2/3 shapes 28x28x128 and
+ * 14x14x256; w_packed from dlq_pack_conv_weights_s8) -> alpha/beta, plus the
  * residual r = the block input x_blk[N][2H][2W][C/2]'s 1x1/s2 downsample
  * (w_ds from dlq_pack_downsample_weights_s8, alpha_ds/beta_ds) requantised to
  * int8 exactly as dlq_conv2d_s2_ds_nhwc_s8 stores y_ds, times res_scale ->

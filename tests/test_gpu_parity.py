@@ -176,7 +176,7 @@ def _dsres_gpu(x, h, w2q, wdq, alpha, beta, alpha_d, beta_d, r_s):
     return nhwc_to_nchw(y.cpu().numpy())
 
 
-@pytest.mark.parametrize("C,H,N", [(128, 28, 3), (256, 14, 5), (512, 7, 37), (128, 28, 1), (512, 7, 9)])
+@pytest.mark.parametrize("C,H,N", [(128, 28, 3), (256, 14, 5), (256, 14, 37), (128, 28, 1), (128, 28, 9)])
 def test_conv2_with_downsample_residual_bitexact(gpu, C, H, N):
     """layerX.0 conv2 (+BN) + the block's 1x1/s2 downsample (+BN, requantised)
     computed in the same launch + ReLU == the oracle's downsample conv, its
@@ -189,7 +189,7 @@ def test_conv2_with_downsample_residual_bitexact(gpu, C, H, N):
     assert np.array_equal(got, ref), f"{np.count_nonzero(got != ref)} int8 mismatches"
 
 
-@pytest.mark.parametrize("C,H,N", [(128, 28, 90), (256, 14, 180), (512, 7, 360)])
+@pytest.mark.parametrize("C,H,N", [(128, 28, 90), (256, 14, 180)])
 def test_conv2_with_downsample_residual_many_items(gpu, C, H, N):
     """The downsample-residual epilogue when every workgroup walks several
     items (the next item's DMA in flight during the epilogue's loads):
@@ -228,19 +228,23 @@ def test_conv2_with_downsample_residual_rejects_bad_shapes(gpu):
     with pytest.raises(DLQError):
         ops.conv2d_dsres_nhwc_s8(h7, w, v, v, torch.zeros((2, 14, 14, 128), dtype=torch.int8, device="cuda"), w, v,
                                  v, 1.0)
+    h7 = torch.zeros((2, 7, 7, 512), dtype=torch.int8, device="cuda")  # layer4.0: the fused stride-2 form only
+    with pytest.raises(DLQError):
+        ops.conv2d_dsres_nhwc_s8(h7, w, v, v, torch.zeros((2, 14, 14, 256), dtype=torch.int8, device="cuda"), w, v,
+                                 v, 1.0)
 
 
 def test_resnet18_downsample_residual_matches_fused_downsample(gpu, knobs):
-    """B=256 forward with the downsample computed in conv2's epilogue (default)
-    (knob ds_split = 1) == the default (the stride-2 launch stores it, conv2
-    reads it)."""
+    """B=256 forward with the layer2.0 / layer3.0 downsample computed in conv2's
+    epilogue (the default) == knob ds_split = -1 (the stride-2 launch stores
+    it, conv2 reads it)."""
     from dlq_amd.models import ResNet18Int8, synthetic_images
     sd, scales = model_and_scales()
     x = synthetic_images(256, seed=23).cuda()
     model = ResNet18Int8(sd, scales, max_batch=256)
-    fused = model(x).cpu().numpy()
-    knobs("ds_split", 1)
     split = model(x).cpu().numpy()
+    knobs("ds_split", -1)
+    fused = model(x).cpu().numpy()
     assert np.array_equal(split.view(np.int32), fused.view(np.int32))
 
 
@@ -389,6 +393,21 @@ def test_resnet18_fused_head_matches_split_head(gpu, knobs):
     knobs("head_split", 1)
     split = model(x).cpu().numpy()
     assert np.array_equal(fused.view(np.int32), split.view(np.int32))
+
+
+@pytest.mark.parametrize("B", [3, 256])
+def test_resnet18_pooled_last_conv_matches_fused_head(gpu, knobs, B):
+    """The last conv pooling its own output (default: conv3x3i GAP, then the
+    FC alone) == knob gap_epi = -1 (the fused gap_fc_kernel head), bit for
+    bit, at a ragged batch (items with absent images) and the bench batch."""
+    from dlq_amd.models import ResNet18Int8, synthetic_images
+    sd, scales = model_and_scales()
+    x = synthetic_images(B, seed=31).cuda()
+    model = ResNet18Int8(sd, scales, max_batch=256)
+    pooled = model(x).cpu().numpy()
+    knobs("gap_epi", -1)
+    fused = model(x).cpu().numpy()
+    assert np.array_equal(pooled.view(np.int32), fused.view(np.int32))
 
 
 def test_im2col_reference_order_bitexact(gpu):

@@ -17,7 +17,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # environment variables libdlq.so reads (capi.cpp knobs) or the child reads
-KNOWN_VARS = {"DLQ_L1_GRID", "DLQ_HEAD_SPLIT", "DLQ_GRAPH", "DLQ_GEMM_TILE", "DLQ_DS_SPLIT", "DLQ_PREFETCH", "DLQ_LIB_PATH"}
+KNOWN_VARS = {"DLQ_L1_GRID", "DLQ_HEAD_SPLIT", "DLQ_GRAPH", "DLQ_GEMM_TILE", "DLQ_DS_SPLIT", "DLQ_PREFETCH", "DLQ_GAP_EPI", "DLQ_LIB_PATH"}
 
 CHILD = r"""
 import json, os, sys, time, torch, numpy as np
