@@ -518,7 +518,12 @@ __global__ __launch_bounds__(SNW * 64, 4) void stem_fused_kernel(StemArgs a) {
 // row and channel where two lanes issued a ds_write_b16 each.  Same item
 // walk, ring, band logic, pooling and numerics as stem_fused_kernel:
 // 61.5-62.8 -> 59.2-60.6 us per launch (four A/B rounds, one box, round 4),
-// bit-identical.
+// bit-identical.  Round 6 cut its loop from ~197 to 160 non-MFMA VALU per
+// step (24 MFMAs): packed multiply / add in the input conversion, packed fma
+// in the requantisation, the pool pad as a min against a per-lane bound, one
+// permlane32 swap without copies, no result selects in the store -- time
+// unchanged (57.02 vs 57.09 us, profiles/r06_ab_stem_valu.txt): the stem is
+// not bound by VALU issue.
 constexpr int S2W = 4;                          // waves: one per column quarter
 constexpr int STG2 = 64 * 16;                   // per wave: [64 oc][16 px] bytes
 constexpr int OFF_STAGE2 = OFF_CR + CR_SLOTS * CR_ROW;
@@ -539,7 +544,8 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
   for (int ot = 0; ot < 2; ++ot)
 #pragma unroll
     for (int t = 0; t < 6; ++t) wr[ot][t] = *(const v4i*)(a.w + (ot * 32 + lr) * SK + t * 32 + lh * 16);
-  const float al[2] = {a.alpha[lr], a.alpha[32 + lr]}, be[2] = {a.beta[lr], a.beta[32 + lr]};
+  using F2 = float __attribute__((ext_vector_type(2)));
+  const F2 ab2[2] = {F2{a.alpha[lr], a.beta[lr]}, F2{a.alpha[32 + lr], a.beta[32 + lr]}};  // (alpha, beta) per channel tile
   for (int i = tid; i < CR_SLOTS * CR_ROW / 16; i += S2W * 64) *(v4i*)(lds + OFF_CR + i * 16) = v4i{0, 0, 0, 0};
   wait_vm_const<0>();
   __syncthreads();
@@ -556,6 +562,10 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
   const int R1 = 16 * tg + 8 * (tg & 1) + (ti >> 1), R2 = 16 * tg + 8 * (1 - (tg & 1)) + (ti >> 1);
   const int8_t* tr1 = stg + R1 * 16 + 8 * ((ti & 1) ^ ((R1 >> 3) & 1));
   const int8_t* tr2 = stg + R2 * 16 + 8 * ((ti & 1) ^ ((R2 >> 3) & 1));
+  // a 16-lane group's transposed reads depend only on its own lanes'
+  // addresses: odd groups read R2's bytes first, so no select on the results
+  const int8_t* trA = (tg & 1) ? tr2 : tr1;
+  const int8_t* trB = (tg & 1) ? tr1 : tr2;
 
   int item0, n_my;
   xcd_chunk(nitems, item0, n_my);
@@ -569,7 +579,6 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
     if (py0 >= py1) continue;
     const int iy0 = 4 * py0 - 5;  // odd: a pair starts on an odd input row
     const float* img = a.x + (size_t)n * 3 * 224 * 224;
-    using F2 = float __attribute__((ext_vector_type(2)));
     F2 raw[PD + 1][2][3];
     __amdgpu_buffer_rsrc_t rs[3];
 #pragma unroll
@@ -610,6 +619,10 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
         v = e == 3 ? sa[(2 * jj + 3) & 7] : v;
         ra[jj][i] = v + 12 - 4 * e;
       }
+    // the scale multiply and the rounding add of a column pair in one packed
+    // instruction each (v_pk_mul_f32 / v_pk_add_f32: the same IEEE products and
+    // sums as two scalar ones), the clamp per value
+    const F2 inv2 = {a.inv_s, a.inv_s}, mg2 = {12582912.0f, 12582912.0f};
     auto convert_quad = [&](const F2 (&r)[2][3], auto jc) {  // jc = (2k) & 7
       constexpr int J = decltype(jc)::value;
       unsigned v[3];
@@ -617,10 +630,14 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
       for (int c = 0; c < 3; ++c) {
         unsigned u[4];
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int d = 0; d < 2; ++d)
-            u[2 * h + d] = __float_as_uint(__builtin_amdgcn_fmed3f(r[h][c][d] * a.inv_s, -127.f, 127.f) + 12582912.0f);
+        for (int h = 0; h < 2; ++h) {
+          // rounding add before the clamp: fl(t + 1.5 2^23) is 1.5 2^23 +
+          // rint(t) for |t| < 2^22 and beyond the clamp bounds otherwise, so
+          // clamping the sum to 1.5 2^23 -+ 127 gives the same bits
+          const F2 t = r[h][c] * inv2 + mg2;
+          u[2 * h] = __float_as_uint(__builtin_amdgcn_fmed3f(t[0], 12582912.0f - 127.f, 12582912.0f + 127.f));
+          u[2 * h + 1] = __float_as_uint(__builtin_amdgcn_fmed3f(t[1], 12582912.0f - 127.f, 12582912.0f + 127.f));
+        }
         v[c] = __builtin_amdgcn_perm(u[1], u[0], 0x0c0c0400u) | __builtin_amdgcn_perm(u[3], u[2], 0x04000c0cu);
       }
 #pragma unroll
@@ -668,13 +685,17 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
 #undef STEM2_WAIT
 #undef STEM2_K
     };
+    // column -1 (the pool's left pad) is masked by a min against the lane's
+    // kb (INT_MIN on the image's left edge, else INT_MAX); lanes 0-31's
+    // column 16 is lanes 32-63's column 0, brought over by one permlane32
+    // swap whose other operand is column 1 (both dead once H[0] is formed)
+    const int kb = (q == 0 && lh == 0) ? kIntMin : 0x7fffffff;
     auto hpool = [&](const v16i& c, int (&H)[8]) {
-      unsigned x0 = (unsigned)c[0], c16 = x0;
-      swap32(x0, c16);
-      const int c0v = (q == 0 && lh == 0) ? kIntMin : c[0];
-      H[0] = max3i(c0v, c[1], c[2]);
+      H[0] = max3i(__builtin_elementwise_min(c[0], kb), c[1], c[2]);
 #pragma unroll
       for (int m = 1; m < 7; ++m) H[m] = max3i(c[2 * m], c[2 * m + 1], c[2 * m + 2]);
+      unsigned x0 = (unsigned)c[0], c16 = (unsigned)c[1];
+      swap32(x0, c16);
       H[7] = max3i(c[14], c[15], (int)c16);
     };
 
@@ -701,11 +722,11 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
       hpool(c[0][0], Hp[0]);
       hpool(c[0][1], Hp[1]);
     }
+    int8_t* const ybase = a.y + ((size_t)n * 56 * 56 + 14 * q + ti) * 64 + 16 * tg;
     auto store_row = [&](int p) {
-      const v2i r1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)tr1);
-      const v2i r2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)tr2);
-      const v4i o = (tg & 1) ? v4i{r2[0], r2[1], r1[0], r1[1]} : v4i{r1[0], r1[1], r2[0], r2[1]};
-      if (ti < 14) *(v4i*)(a.y + (((size_t)n * 56 + p) * 56 + 14 * q + ti) * 64 + 16 * tg) = o;
+      const v2i r1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)trA);
+      const v2i r2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)trB);
+      if (ti < 14) *(v4i*)(ybase + p * 56 * 64) = v4i{r1[0], r1[1], r2[0], r2[1]};
     };
     auto step = [&](int t, auto setc) {
       constexpr int S = decltype(setc)::value;
@@ -724,11 +745,18 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
         hpool(c[1][ot], Ho);
         unsigned w[2] = {0u, 0u};
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          const int v = max3i(Hp[ot][m], He[m], Ho[m]);
+        // two pooled values per v_pk_fma_f32 (the builtin: an inline-asm form
+        // broadcasting alpha / beta by op_sel saved 4 VGPRs but gave ~25
+        // differing bytes per B = 256 launch from run to run -- a hazard the
+        // compiler does not see through asm; tools/probe/stem_det.py)
+        for (int m = 0; m < 8; m += 2) {
+          const int v0 = max3i(Hp[ot][m], He[m], Ho[m]), v1 = max3i(Hp[ot][m + 1], He[m + 1], Ho[m + 1]);
           Hp[ot][m] = Ho[m];
-          const float y = __builtin_fmaf((float)v, al[ot], be[ot]);
-          w[m >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_fminf(y, 127.f), m & 3, w[m >> 2]);
+          Hp[ot][m + 1] = Ho[m + 1];
+          const F2 y = __builtin_elementwise_fma(F2{(float)v0, (float)v1}, F2{ab2[ot][0], ab2[ot][0]}, F2{ab2[ot][1], ab2[ot][1]});
+          const float y0 = __builtin_fminf(y[0], 127.f), y1 = __builtin_fminf(y[1], 127.f);
+          w[m >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(y0, m & 3, w[m >> 2]);
+          w[m >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(y1, (m + 1) & 3, w[m >> 2]);
         }
         const int row = ot * 32 + lr;
         *(v2i*)(stg + row * 16 + 8 * (lh ^ ((row >> 3) & 1))) = v2i{(int)w[0], (int)w[1]};
