@@ -123,6 +123,19 @@ struct DsrGeo {
   static __device__ __forceinline__ int swz(int lp) { return NCH == 4 ? (lp >> 2) & 3 : (lp >> 1) & 7; }
 };
 
+// The loaded residual staged in LDS (conv3x3i_body RLDS, 28x28 / 14x14): the
+// item's 392 pixels x 128 channels, DMA'd during its second-last stage and
+// read by the epilogue; pixel lp's 16-byte chunk c at lp * 128 + 16 (c ^
+// ((lp >> 1) & 7)), so a ds_read_b128 lane group (16 pixels, one chunk) hits
+// 16 distinct bank quads.
+template <int W, int C>
+struct ResGeo {
+  using G = IGeo<W, 1>;
+  static constexpr int OFF_RES = G::OFF_AB + 2 * C * 4;
+  static constexpr int NPR = IL * G::OT / 1024;      // LDS-DMA pieces (49; W = 7 has no RLDS)
+  static constexpr int LDS_END = OFF_RES + NPR * 1024;
+};
+
 // Wave -> (oc tile, first px tile, px tile count).  MT = 4: SIMD pair (w, w+4)
 // = oc tile w&3, tiles [0,7) and [7,13).  MT = 2: oc tile w&1, tile groups
 // [0,4) [4,7) [7,10) [10,13) by w>>1, so the pair (w, w+4) owns 7 or 6.
@@ -307,6 +320,10 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
   static_assert(!GAP || (W == 7 && C == 512 && OUT == 0 && !F8), "the pooled head follows the 7x7x512 conv");
   static_assert(!DSR || (OUT == 0 && RES && RELU && !F8 && W != 7), "the downsample residual: int8 ReLU, 28x28 / 14x14");
   constexpr bool RESL = RES && !DSR;  // the residual is loaded (DSR: computed)
+  // ... through LDS (RLDS: 28x28 / 14x14 int8, where it fits beside the ring),
+  // else into registers at the item's last k-step
+  constexpr bool RLDS = RESL && !F8 && !GAP && W != 7 && OUT == 0;
+  using RG = ResGeo<W, C>;
   constexpr int KD = C / 64;          // DSR: downsample k-steps (the block input has C/2 channels)
   using DG = DsrGeo<W, C>;
   constexpr int SPS = sps_of<W, F8>();
@@ -409,6 +426,15 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       for (int kk = 0; kk < (DSR ? KD : 1); ++kk)
         ads[kk] = gload16_untracked(a.ds_w + ((size_t)((o >> 7) * KD + kk) * 128 + (o & 127)) * 48 + lh * 16);
     };
+    if constexpr (RLDS) {
+      if (j == NS - 2) {  // the item's residual, landed by the next stage's wait + barrier
+        for (int pc = wave; pc < RG::NPR; pc += INW) {
+          const int u = pc * 64 + lane, lp = u >> 3, c = (u & 7) ^ ((lp >> 1) & 7), p = cur_p0 + lp;
+          const int8_t* src = p < a.P ? a.res + (size_t)p * a.OC + cur_ot * G::OT + c * 16 : g_zero_i + (lane & 3) * 16;
+          glds16_asm(src, lds_addr32(lds) + RG::OFF_RES + pc * 1024);
+        }
+      }
+    }
     if constexpr (DSR) {
       if (j == NS - 2) {
         // the item's block-input pixels and downsample alpha / beta (piece
@@ -533,7 +559,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
         acc[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu], fb[bu][f], acc[f], 0, 0, 0);
         if (f == NF - 1 && ks + 2 < KSN) fa[bu] = a_at(ks + 2);
         if (ks + 2 < KSN && !DLQ_ABL(a, 8)) ld_b(ks + 2, f);  // probe builds: dbg 8 re-uses k-steps 0/1's B
-        if constexpr (OUT == 0 && RESL) {
+        if constexpr (OUT == 0 && RESL && !RLDS) {
           if (ks == KSN - 1 && j == NS - 1) res_load(f);
         }
       }
@@ -578,7 +604,7 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
       for (int f = 0; f < NF; ++f) {
         acc[f] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[bu], fb[f], acc[f], 0, 0, 0);
         if (ks + 1 < KSN && !DLQ_ABL(a, 8)) ld_b(ks + 1, f);  // probe builds: dbg 8 re-uses k-step 0's B
-        if constexpr (OUT == 0 && RESL) {
+        if constexpr (OUT == 0 && RESL && !RLDS) {
           // into the registers this tile's last B fragment just freed
           if (ks == KSN - 1 && j == NS - 1) res_load(f);
         }
@@ -705,9 +731,15 @@ __device__ __forceinline__ void conv3x3i_body(const ConvArgs& a, int8_t* lds, in
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
         unsigned r[4] = {0, 0, 0, 0};
-        if constexpr (RES) {
+        if constexpr (RLDS) {
+          int lp = (f0 + f) * 32 + lr;
+          lp = lp < IL ? lp : IL - 1;
+          rq[f] = *(const v4i*)(lds + RG::OFF_RES + lp * 128 + (((2 * mt + lh) ^ ((lp >> 1) & 7)) << 4));
+        } else if constexpr (RES) {
           // younger than rq[f]: rq[f+1..NF-1] and the stores of tiles 0..f-1
           asm volatile("s_waitcnt vmcnt(%1)" : "+v"(rq[f]) : "n"(NF - 1) : "memory");
+        }
+        if constexpr (RES) {
           r[0] = (unsigned)rq[f][0];
           r[1] = (unsigned)rq[f][1];
           r[2] = (unsigned)rq[f][2];
@@ -818,7 +850,8 @@ template <int W, int C, int OUT, bool RES, bool F8 = false, bool RELU = false, b
 __global__ __launch_bounds__(INW * 64, 1) void conv3x3i_kernel(ConvArgs a) {
   using G = IGeo<W, sps_of<W, F8>()>;
   constexpr int OFF_AB = G::OFF_AB;
-  constexpr int LDS_TOTAL = DSR ? DsrGeo<W, C>::LDS_END : OFF_AB + 2 * C * 4;
+  constexpr bool RLDS = RES && !DSR && !F8 && !GAP && W != 7 && OUT == 0;
+  constexpr int LDS_TOTAL = DSR ? DsrGeo<W, C>::LDS_END : RLDS ? ResGeo<W, C>::LDS_END : OFF_AB + 2 * C * 4;
   static_assert(LDS_TOTAL <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) int8_t lds[LDS_TOTAL];
   const int tid = threadIdx.x;

@@ -214,8 +214,11 @@ constexpr int GK2 = 128;
 
 // Tile TM x TN per workgroup of WM x WN waves, each wave MI x NJ MFMA tiles
 // (32 x 32); TM = 32 WM MI, TN = 32 WN NJ.  Per stage K = 128: TM / 8 A
-// pieces (8 rows x 128 K bytes each) and TN / 8 B pieces (1024 / TN K rows x
-// TN bytes each), dealt to the waves round-robin.
+// pieces (8 rows x 128 K bytes each) and TNP / 8 B pieces (1024 / TNP K rows
+// x TNP bytes each), dealt to the waves round-robin (a wave whose last slot
+// index passes the piece count issues nothing there: wave-uniform).  TNP =
+// TN but 256 for TN = 224 (7 MFMA columns): the B image keeps the 256-byte
+// row pitch and swizzle, its two spare chunks per row read zeros.
 //  * A image: row m = 128 K bytes, chunk c at m*128 + 16*(c ^ ((m >> 1) & 7)).
 //  * B image: K rows of TN bytes as loaded: chunk b of row k at k*TN +
 //    16*(b ^ swz(k)), swz(k) = 2(k & 7) for TN = 256 and 2((k >> 1) & 3) for
@@ -224,6 +227,10 @@ constexpr int GK2 = 128;
 template <int TN>
 __device__ __forceinline__ int bswz(int k) {
   return TN == 256 ? 2 * (k & 7) : 2 * ((k >> 1) & 3);
+}
+template <int TN>
+constexpr int b_pitch() {  // B image row pitch (NN) / staged rows (NT)
+  return TN == 224 ? 256 : TN;
 }
 
 // BT: B supplied transposed (Bt[N][K]): its tile is staged and read exactly
@@ -239,10 +246,10 @@ template <int WM, int WN, int MI, int NJ, bool BT>
 __device__ __forceinline__ void k128_tile(const int8_t* __restrict__ A, const int8_t* __restrict__ B, int M, int N,
                                           int K, int m0, int n0, int sb, int se, int8_t* lds,
                                           v16i (&acc)[MI][NJ]) {
-  constexpr int NW = WM * WN, TM = 32 * WM * MI, TN = 32 * WN * NJ;
-  constexpr int SA = TM * GK2, SLOT = SA + GK2 * TN;  // slot: A image, then B image
-  constexpr int PA = TM / 8, PB = TN / 8, NP = PA + PB, PPW = NP / NW;  // pieces: A, B, per wave
-  constexpr int CPR = TN / 16;  // B chunks per K row
+  constexpr int NW = WM * WN, TM = 32 * WM * MI, TN = 32 * WN * NJ, TNP = b_pitch<TN>();
+  constexpr int SA = TM * GK2, SLOT = SA + GK2 * TNP;  // slot: A image, then B image
+  constexpr int PA = TM / 8, PB = TNP / 8, NP = PA + PB, PPW = (NP + NW - 1) / NW;  // pieces: A, B, per wave
+  constexpr int CPR = TNP / 16;  // B chunks per K row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 31, lh = lane >> 5;
   const int wm = wave / WN, wn = wave % WN;
@@ -257,18 +264,19 @@ __device__ __forceinline__ void k128_tile(const int8_t* __restrict__ A, const in
     const int k0 = st * GK2;
     const unsigned slot = lds32 + (st & 1) * SLOT;
     const int pc = wave + NW * r;
+    if (NP % NW != 0 && pc >= NP) return;  // wave-uniform: no piece in this slot
     if (pc < PA) {
       const int m = 8 * pc + (lane >> 3), c = (lane & 7) ^ ((m >> 1) & 7), k = k0 + 16 * c;
       const int8_t* src = (m0 + m < M && k < kend) ? A + (size_t)(m0 + m) * K + k : zsrc;
       glds16_asm(src, slot + pc * 1024);
     } else if constexpr (BT) {
       const int q = pc - PA, n = 8 * q + (lane >> 3), c = (lane & 7) ^ ((n >> 1) & 7), k = k0 + 16 * c;
-      const int8_t* src = (n0 + n < N && k < kend) ? B + (size_t)(n0 + n) * K + k : zsrc;
+      const int8_t* src = (n < TN && n0 + n < N && k < kend) ? B + (size_t)(n0 + n) * K + k : zsrc;
       glds16_asm(src, slot + SA + q * 1024);
     } else {
-      const int q = pc - PA, k = (1024 / TN) * q + lane / CPR;
-      const int b = (lane % CPR) ^ bswz<TN>(k), n = n0 + 16 * b;
-      const int8_t* src = (k0 + k < kend && n < N) ? B + (size_t)(k0 + k) * N + n : zsrc;
+      const int q = pc - PA, k = (1024 / TNP) * q + lane / CPR;
+      const int b = (lane % CPR) ^ bswz<TNP>(k), n = n0 + 16 * b;
+      const int8_t* src = (16 * b < TN && k0 + k < kend && n < N) ? B + (size_t)(k0 + k) * N + n : zsrc;
       glds16_asm(src, slot + SA + q * 1024);
     }
   };
@@ -301,8 +309,8 @@ __device__ __forceinline__ void k128_tile(const int8_t* __restrict__ A, const in
           fb[j] = *(const v4i*)(lb + n * 128 + 16 * (c ^ ((n >> 1) & 7)));
         } else {
           const int k = ks * 32 + lh * 16 + q, b = (wn * NJ + j) * 2 + g;
-          const int8_t* a0 = lb + k * TN + 16 * (b ^ bswz<TN>(k)) + 8 * p;
-          const v2i lo = ds_tr8(a0), hi = ds_tr8(a0 + 8 * TN);
+          const int8_t* a0 = lb + k * TNP + 16 * (b ^ bswz<TNP>(k)) + 8 * p;
+          const v2i lo = ds_tr8(a0), hi = ds_tr8(a0 + 8 * TNP);
           fb[j] = v4i{lo[0], lo[1], hi[0], hi[1]};
         }
       }
@@ -351,11 +359,12 @@ __global__ __launch_bounds__(WM * WN * 64, WPS) void gemm_s8s8s32_k128_kernel(co
                                                                              const int8_t* __restrict__ B,
                                                                              int32_t* __restrict__ C, int M, int N,
                                                                              int K, int nbn) {
-  constexpr int NW = WM * WN, TM = 32 * WM * MI, TN = 32 * WN * NJ;
-  static_assert(TN == 256 || TN == 128, "B image swizzle");
-  constexpr int SA = TM * GK2, SLOT = SA + GK2 * TN;
-  constexpr int PA = TM / 8, PB = TN / 8, NP = PA + PB, PPW = NP / NW;
-  static_assert(NP % NW == 0 && PPW <= 4 * MI * NJ, "at most one piece per MFMA of a stage");
+  constexpr int NW = WM * WN, TM = 32 * WM * MI, TN = 32 * WN * NJ, TNP = b_pitch<TN>();
+  static_assert(TNP == 256 || TNP == 128, "B image swizzle");
+  constexpr int SA = TM * GK2, SLOT = SA + GK2 * TNP;
+  constexpr int PA = TM / 8, PB = TNP / 8, NP = PA + PB, PPW = (NP + NW - 1) / NW;
+  static_assert(PPW <= 4 * MI * NJ, "at most one piece per MFMA of a stage");
+  static_assert(2 * SLOT <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) int8_t lds[2 * SLOT];
   // tile order: each XCD takes a contiguous run of l (xcd_remap), and l runs
   // down groups of GROW row blocks column by column, so the tiles an XCD's
@@ -391,9 +400,10 @@ int num_cus_gemm() {
 // 12544 x 512 x 4608 1009 / 1497 / 1374 (98 tiles of 256 x 256 idle 60 % of
 // the chip); 128 x 200704 x 1152 655 / 585 / 775 (half of a 256-row tile
 // would be padding).
+// Tiles 4-6 have a 7-MFMA side (224): 256 x 224, 224 x 128, 224 x 256.
 int gemm_tile_for(int M, int N) {
   const int forced = g_knob_gemm_tile.load(std::memory_order_relaxed);
-  if (forced >= 1 && forced <= 3) return forced;
+  if (forced >= 1 && forced <= 6) return forced;
   if (M <= 128) return 3;
   const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
   if (t256 >= num_cus_gemm() || M <= 256 || N <= 256) return 1;
@@ -407,7 +417,8 @@ hipError_t launch_gemm(const int8_t* A, const int8_t* B, int32_t* C, int M, int 
   const bool dma = K % 16 == 0 && (BT || N % 16 == 0) && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0;
   if (dma) {
     const int cfg = gemm_tile_for(M, N);
-    const int TM = cfg == 3 ? 128 : 256, TN = cfg == 1 ? 256 : 128;
+    static const int TMS[7] = {0, 256, 256, 128, 256, 224, 224}, TNS[7] = {0, 256, 128, 128, 224, 128, 256};
+    const int TM = TMS[cfg], TN = TNS[cfg];
     const long tiles = (long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     const int nbn = (N + TN - 1) / TN;
@@ -417,8 +428,17 @@ hipError_t launch_gemm(const int8_t* A, const int8_t* B, int32_t* C, int M, int 
     else if (cfg == 2)
       hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<4, 2, 2, 2, 1, BT>), dim3((unsigned)tiles), dim3(512), 0, s, A, B, C,
                          M, N, K, nbn);
-    else
+    else if (cfg == 3)
       hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<2, 2, 2, 2, 2, BT>), dim3((unsigned)tiles), dim3(256), 0, s, A, B, C,
+                         M, N, K, nbn);
+    else if (cfg == 4)
+      hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<8, 1, 1, 7, 1, BT>), dim3((unsigned)tiles), dim3(512), 0, s, A, B, C,
+                         M, N, K, nbn);
+    else if (cfg == 5)
+      hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<1, 4, 7, 1, 1, BT>), dim3((unsigned)tiles), dim3(256), 0, s, A, B, C,
+                         M, N, K, nbn);
+    else
+      hipLaunchKernelGGL((gemm_s8s8s32_k128_kernel<1, 8, 7, 1, 1, BT>), dim3((unsigned)tiles), dim3(512), 0, s, A, B, C,
                          M, N, K, nbn);
   } else {
     const int nbm = (M + GT - 1) / GT, nbn = (N + GT - 1) / GT;

@@ -116,7 +116,8 @@ int dlq_pack_conv_weights_s8(const dlq_conv_desc* d, const int8_t* q_oihw, int I
  *   "head_split" (DLQ_HEAD_SPLIT) 1 = GAP and FC as two launches;
  *   "graph"      (DLQ_GRAPH)      1 = replay the forward as a hipGraph;
  *   "gemm_tile"  (DLQ_GEMM_TILE)  dlq_gemm_s8s8s32's tile, 0 = by shape,
- *                                 1 = 256 x 256, 2 = 256 x 128, 3 = 128 x 128;
+ *                                 1 = 256 x 256, 2 = 256 x 128, 3 = 128 x 128,
+ *                                 4 = 256 x 224, 5 = 224 x 128, 6 = 224 x 256;
  *   "ds_split"   (DLQ_DS_SPLIT)   0 = (default) the engine computes the
  *                                 layer2.0 / layer3.0 1x1/s2 downsample in
  *                                 their conv2 launch (dlq_conv2d_dsres_nhwc_s8);

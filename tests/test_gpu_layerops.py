@@ -78,12 +78,13 @@ def test_gemm_s8s8s32_reference_layout(gpu, M, N, K):
     assert np.array_equal(Cd.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 528, 2304), (257, 400, 80), (130, 1040, 4608),
-                                   (513, 144, 16), (2304, 4096, 144)])
+                                   (513, 144, 16), (2304, 4096, 144), (448, 672, 384), (225, 225, 272)])
 def test_gemm_s8s8s32_every_tile_shape(gpu, knobs, tile, M, N, K):
     """Each tile of the LDS-DMA kernel (knob gemm_tile: 1 = 256 x 256, 2 = 256 x
-    128, 3 = 128 x 128; by default chosen by shape) on whole tiles, M / N / K
+    128, 3 = 128 x 128, 4 = 256 x 224, 5 = 224 x 128, 6 = 224 x 256; by
+    default chosen by shape) on whole tiles, M / N / K
     tails and K below one stage, and a grid of several tiles per CU in the
     grouped raster (2304 x 4096: 9 row blocks = two full groups of 4 and a
     group of 1) -- bit-exact with the oracle."""
@@ -130,7 +131,7 @@ def test_gemm_s8s8s32_kernel_selection(gpu, M, N, K, a_off, b_off):
     assert np.array_equal(Cd.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("M,N,K,a_off,b_off", [(256, 256, 128, 0, 0), (300, 521, 2304, 0, 0), (257, 400, 80, 0, 0),
                                                (130, 1040, 4608, 0, 0), (513, 7, 16, 0, 0), (100, 77, 61, 0, 0),
                                                (33, 65, 1, 0, 0), (300, 520, 128, 0, 8), (130, 264, 96, 3, 5)])

@@ -1,6 +1,6 @@
 """dlq_gemm_s8s8s32 (NN: B[K][N]) and dlq_gemm_s8s8s32_nt (NT: Bt[N][K]) TOPS
 per tile configuration (knob gemm_tile 0 = the by-shape choice, 1 = 256 x 256,
-2 = 256 x 128, 3 = 128 x 128) on the bench's GEMM shapes and the conv-shaped
+2 = 256 x 128, 3 = 128 x 128, 4 = 256 x 224, 5 = 224 x 128, 6 = 224 x 256) on the bench's GEMM shapes and the conv-shaped
 calibration cases: hipEvents over back-to-back calls, one process.  Every
 configuration is timed in ROUNDS rounds whose order rotates (the first
 configuration timed in a process used to read low: the clock ramp), after a
@@ -27,7 +27,7 @@ for (M, N, K) in ((8192, 8192, 8192), (4096, 4096, 4096), (256, 50176, 2304), (1
     C = torch.empty((M, N), dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream().cuda_stream
     res = {}
-    configs = [(lay, t) for lay in ("nn", "nt") for t in (0, 1, 2, 3)]
+    configs = [(lay, t) for lay in ("nn", "nt") for t in (0, 1, 2, 3, 4, 5, 6)]
     times = {f"{lay}{t}": [] for lay, t in configs}
     st = torch.cuda.current_stream().cuda_stream
 
