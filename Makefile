@@ -42,7 +42,11 @@ build/plancap%.o: tools/check/plan_capture.hip dlq_amd/csrc/conv3x3i.hip dlq_amd
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -DPLANCAP_KIND=$* -I dlq_amd/csrc -c -o $@ $<
 
-tools/check/libplancap.so: build/plancap0.o build/plancap1.o
+build/dmamask.o: tools/check/dma_mask_check.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -I dlq_amd/csrc -c -o $@ $<
+
+tools/check/libplancap.so: build/plancap0.o build/plancap1.o build/dmamask.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle:

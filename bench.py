@@ -299,7 +299,7 @@ def timed_cuda(fn, iters, warmup=3):
     return a.elapsed_time(b) / iters
 
 
-def extra_configs(dev):
+def extra_configs(dev, cal_images=32):
     """BASELINE configs[0], [1] and [4] and the exported GEMM, each measured
     after the headline's timed region (rank 0, N = 1)."""
     from dlq_amd.models import MLPInt8, MNISTMLP, ResNet18Int8, mlp_weights, mnist_inputs, resnet18_state_dict
@@ -414,6 +414,9 @@ def extra_configs(dev):
         sd = resnet18_state_dict(SEED)
         sc8 = calibrate_resnet18(sd, synthetic_images(2, seed=SEED + 1), device="cpu", qmax=448.0)
         m8 = ResNet18Int8(sd, sc8, max_batch=256, precision="fp8")
+        # the headline's calibration: the GPU fp32 reference over the same
+        # --cal-images set (the CPU pass above only seeds the model)
+        m8.calibrate(synthetic_images(cal_images, seed=SEED + 1).to(dev).contiguous(), 448.0)
         g = torch.Generator(device=dev).manual_seed(SEED + 2000)
         x8 = (torch.rand((256, 3, 224, 224), generator=g, device=dev) * 4.0 - 2.0).contiguous()
         lg = torch.empty((256, 1000), dtype=torch.float32, device=dev)
@@ -423,7 +426,8 @@ def extra_configs(dev):
             "value": round(256 / (ms * 1e-3), 1), "unit": "images/s", "ms_per_forward": round(ms, 4),
             "tflops": round(2 * (c_macs + f_macs) * 256 / (ms * 1e-3) / 1e12, 1),
             "frac_of_fp8_peak": round(2 * (c_macs + f_macs) * 256 / (ms * 1e-3) / 1e12 / PEAK_I8_TOPS, 4),
-            "timing": "torch events around 20 forwards after 5 warmup, B = 256, inputs resident"}
+            "timing": "torch events around 20 forwards after 5 warmup, B = 256, inputs resident",
+            "calibration": f"e4m3 scales from the GPU fp32 reference over {cal_images} seeded images, as the headline"}
         del m8
     except Exception as e:
         out["configs[4] error"] = repr(e)
@@ -600,7 +604,7 @@ def main():
         except Exception as e:  # baseline is reported context, never fatal
             out["cpu_baseline_error"] = repr(e)
         if args.extras and not fp8:
-            out["extra_configs"] = extra_configs(dev)
+            out["extra_configs"] = extra_configs(dev, args.cal_images)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -96,7 +96,15 @@ def test_spawn_ranks_kills_children_on_interrupt(tmp_path):
         f"sys.path.insert(0, {ROOT!r})\n"
         "import bench, subprocess\n"
         "bench.__file__ = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'child.py')\n"
-        "threading.Timer(2.0, lambda: os.kill(os.getpid(), signal.SIGTERM)).start()\n"
+        "def _term():\n"
+        "    import time\n"
+        "    d = os.path.dirname(os.path.abspath(__file__))\n"
+        "    t0 = time.time()\n"
+        "    ok = lambda f: os.path.exists(f) and os.path.getsize(f) > 0\n"
+        "    while time.time() - t0 < 50 and not all(ok(os.path.join(d, 'pid%d' % r)) for r in (0, 1)):\n"
+        "        time.sleep(0.05)\n"
+        "    os.kill(os.getpid(), signal.SIGTERM)\n"
+        "threading.Thread(target=_term, daemon=True).start()\n"
         "sys.exit(bench.spawn_ranks(2))\n")
     (tmp_path / "child.py").write_text(
         "import os, time\n"
@@ -106,6 +114,7 @@ def test_spawn_ranks_kills_children_on_interrupt(tmp_path):
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 128 + 15, r.stderr[-2000:]
     for rank in (0, 1):
+        assert (tmp_path / f"pid{rank}").exists(), f"rank {rank} never started (pid file missing)"
         pid = int((tmp_path / f"pid{rank}").read_text())
         alive = True
         try:

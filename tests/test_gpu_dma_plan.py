@@ -96,3 +96,26 @@ def test_stride2_conv_plan_is_the_kernels(gpu, OW, N):
     n, cnt, lds, src, bases = _capture(1, 2 * OW, N)
     sizes = (N * 4 * OW * OW * C_, (C_ // 32) * 2 * C_ * 304, (C_ // 32) * 2 * C_ * 48)
     _compare(emit, n, cnt, lds, src, bases, sizes, f"conv3x3s2i OW={OW} N={N}")
+
+
+def test_masked_lds_dma(gpu):
+    """The masked LDS-DMA issues the kernels' shared piece plans use for empty
+    slots (device_common.h glds16_asm_m / glds16_saddr_m), run for real
+    (tools/check/dma_mask_check.hip, compiled without DLQ_PLAN_CAPTURE): with
+    valid = false neither form writes its LDS piece (the poison stays), with
+    valid = true both land their 1 KiB, and every lane stores after each
+    (EXEC restored).  The conv tests cannot see this: an empty slot re-issues
+    another wave's piece, identical bytes to the same address."""
+    import torch
+    if not os.path.exists(LIB):
+        pytest.fail(f"{LIB} missing: build it with `make` (Makefile target tools/check/libplancap.so)")
+    lib = C.CDLL(LIB)
+    lib.dmamask_run.restype = C.c_int
+    src = torch.arange(4096, dtype=torch.int32, device="cuda").remainder(251).to(torch.int8)
+    out = torch.zeros(4096, dtype=torch.int8, device="cuda")
+    lanes = torch.zeros(256, dtype=torch.int32, device="cuda")
+    assert lib.dmamask_run(C.c_void_p(src.data_ptr()), C.c_void_p(out.data_ptr()), C.c_void_p(lanes.data_ptr())) == 0
+    o, s = out.cpu().numpy(), src.cpu().numpy()
+    assert (o[:2048].view(np.uint8) == 0xA5).all(), "a masked (valid = false) piece wrote LDS"
+    assert np.array_equal(o[2048:], s[2048:]), "an unmasked piece did not land"
+    assert np.array_equal(lanes.cpu().numpy(), np.tile(np.arange(1, 65, dtype=np.int32), 4)), "EXEC not restored"

@@ -55,6 +55,14 @@ extern "C" int PLANCAP_RUN(int kind, int W, int N, unsigned max_rec, unsigned* c
   float* ab = nullptr;
   PlanPiece* buf = nullptr;
   unsigned* dcnt = nullptr;
+  struct FreeAll {  // every exit path (HIP error, dropped pieces, success) frees the buffers
+    void* const* p[8];
+    ~FreeAll() {
+      for (void* const* q : p)
+        if (*q) (void)hipFree(*q);
+    }
+  } free_all{{(void* const*)&x, (void* const*)&w, (void* const*)&wd, (void* const*)&y, (void* const*)&yd,
+               (void* const*)&ab, (void* const*)&buf, (void* const*)&dcnt}};
   const int items = kind == 0 ? (OC / (OW == 7 ? 64 : 128)) * ((P + 391) / 392) : (OC / 128) * ((P + 195) / 196);
   // the launchers' grid: min(items, CUs) (num_cus_i / num_cus_s2i)
   int dev = 0, ncu = 0;
@@ -118,7 +126,5 @@ extern "C" int PLANCAP_RUN(int kind, int W, int N, unsigned max_rec, unsigned* c
   bases[1] = (uintptr_t)w;
   bases[2] = (uintptr_t)wd;
   bases[3] = (uintptr_t)zero;
-  for (void* p : {(void*)x, (void*)w, (void*)wd, (void*)y, (void*)yd, (void*)ab, (void*)buf, (void*)dcnt})
-    (void)hipFree(p);
   return nw;
 }
