@@ -537,6 +537,7 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;  // q = column quarter = wave
   const int lr = lane & 31, lh = lane >> 5;
   const int nitems = a.N * a.nb;
+  ST_DECL;
 
   // both channel tiles' weight fragments and epilogue constants, in registers
   v4i wr[2][6];
@@ -733,11 +734,15 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
       const int p = py0 + t;
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_s_barrier();
+      ST(0);
       v16i c[2][2];
       conv_rows2(2 * p, c);
+      ST(2);
       convert_quad(raw[(S + 3) % (PD + 1)], std::integral_constant<int, (2 * S + 6) & 7>{});
+      ST(1);
       if (t > 0) store_row(p - 1);
       load_quad(t + 3 + PD, raw[(S + 2) % (PD + 1)]);
+      ST(4);
 #pragma unroll
       for (int ot = 0; ot < 2; ++ot) {
         int He[8], Ho[8];
@@ -761,8 +766,10 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
         const int row = ot * 32 + lr;
         *(v2i*)(stg + row * 16 + 8 * (lh ^ ((row >> 3) & 1))) = v2i{(int)w[0], (int)w[1]};
       }
+      ST(3);
     };
     const int nsteps = py1 - py0;
+    ST(5);
     static_assert(PD == 3, "the step loop below is unrolled by 4");
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -782,6 +789,7 @@ __global__ __launch_bounds__(S2W * 64, 2) void stem2_kernel(StemArgs a) {
     wait_vm0();
     __syncthreads();
   }
+  ST_STORE();
 }
 
 int num_cus_stem() {

@@ -39,7 +39,7 @@ int main(int argc, char** argv) {
   for (int blk : {0, 100})
     for (int wv = 0; wv < 8; ++wv) {
       const unsigned long long* p = &s[(blk * 8 + wv) * 8];
-      printf("blk %3d w%d: barrier %7llu convert %7llu issue %6llu mfma+hpool %7llu epi+store %7llu top %6llu\n", blk,
+      printf("blk %3d w%d: barrier %7llu convert %7llu mfma-issue %6llu pool+epi %7llu store+load %7llu prologue %6llu\n", blk,
              wv, p[0], p[1], p[2], p[3], p[4], p[5]);
     }
 #endif
