@@ -8,6 +8,9 @@
 #include <cstdlib>
 #include <vector>
 #include "../../dlq_amd/csrc/block_l1.hip"
+namespace dlq {
+std::atomic<int> g_knob_l1_grid{0};  // capi.cpp's knob (the probe links no library)
+}
 
 using namespace dlq;
 int main(int argc, char** argv) {
