@@ -228,7 +228,11 @@ bool head_split() { return g_knob_head_split.load(std::memory_order_relaxed) == 
 // layer2.0 and layer3.0) and its stride-2 conv1 runs alone, instead of the
 // downsample fused into the stride-2 launch (conv3x3s2i DS, stored and read
 // back as conv2's residual; layer4.0 always, or every block with -1).
-bool ds_split() { return g_knob_ds_split.load(std::memory_order_relaxed) >= 0; }
+// 1 / 2: only layer3.0 (14x14 output) / only layer2.0 (28x28) (A/B of the two)
+bool ds_split(int OH) {
+  const int k = g_knob_ds_split.load(std::memory_order_relaxed);
+  return k == 0 || (k == 1 && OH == 14) || (k == 2 && OH == 28) || k > 2;
+}
 
 // Knob "prefetch" (DLQ_PREFETCH): 0 = default on, -1 = off.  Each wide /
 // stride-2 conv launch's last stage reads the next launch's first weight
@@ -349,7 +353,7 @@ int basic_block_forward(dlq_resnet18* m, const Block& b, const int8_t* in, int N
     return DLQ_OK;
   }
   const ConvLayer* c2w = &m->convs[b.c2];
-  if (b.down && m->convs[b.ds].wf && ds_split() && conv3x3s2_shape(c1.Cstore, c1.OC, H, W, 3, 3, 2, 2, 1, 1) &&
+  if (b.down && m->convs[b.ds].wf && ds_split(H / 2) && conv3x3s2_shape(c1.Cstore, c1.OC, H, W, 3, 3, 2, 2, 1, 1) &&
       wide_layout(c1.Cstore, c1.OC, H, W, 3, 3, 2, 2, 1, 1) &&
       conv3x3w_shape(c2w->Cstore, c2w->OC, H / 2, W / 2, 3, 3, 1, 1, 1, 1) && H / 2 != 7 && c2w->Cstore == c1.OC &&
       m->convs[b.ds].OC == c1.OC && 2 * c1.Cstore == c1.OC) {

@@ -123,6 +123,7 @@ int dlq_pack_conv_weights_s8(const dlq_conv_desc* d, const int8_t* q_oihw, int I
  *                                 their conv2 launch (dlq_conv2d_dsres_nhwc_s8);
  *                                 -1 = fused into the stride-2 conv1 launch
  *                                 (dlq_conv2d_s2_ds_nhwc_s8) as for layer4.0;
+ *                                 1 / 2 = in conv2 for layer3.0 / layer2.0 only;
  *   "prefetch"   (DLQ_PREFETCH)   0 = (default) each launch of a forward
  *                                 reads the next launch's first weights during
  *                                 its last stage; -1 = off;
