@@ -26,8 +26,8 @@ DLQ_PREC_INT8, DLQ_PREC_FP8 = 0, 1
 # (the first word names the int8 forward's kernel; the fp8 forward runs
 # stem_fused_kernel and block_l1_kernel in families 0 and 1)
 FAMILIES = ["stem2_kernel (int8 stem; fp8: stem_fused_kernel)",
-            "block_l1_sp_kernel (int8 layer1 block; fp8: block_l1_kernel)", "conv3x3s2i_kernel (+downsample)",
-            "conv3x3i_kernel (layer2-4 s1)", "head: gap_fc_kernel (int8 GAP+FC) / gap16 (fp8, split)", "linear_kernel (fc: fp8 / split head)", "other",
+            "block_l1_sp_kernel (int8 layer1 block; fp8: block_l1_kernel)", "conv3x3s2i_kernel (layer2-4 .0 conv1; + downsample at layer4.0)",
+            "conv3x3i_kernel (layer2-4 s1)", "head: gap_fc_kernel (int8 GAP+FC) / gap16 (fp8, split)", "linear_kernel (FC on the pooled codes; fp8 / split head)", "other",
             "conv_s8_kernel fp8 (all convs, fp8 path)"]
 
 
