@@ -2,7 +2,7 @@
 // downsample kernel (conv3x3s2i.hip) on the three ResNet-18 shapes, random
 // int8 data, B = 256; argv: OW (28/14/7), dbg bits (2 = no LDS-DMA, 4 = no
 // epilogues, 8 = no downsample epilogue, 16 / 32 = downsample / conv1 stores
-// to a trash line).
+// to a trash line), ds (1 default; 0 = conv1 alone).
 // With -DDLQ_STAMPS it also prints per-wave s_memtime stamps (prologue,
 // per-stage barrier wait / MFMA loop, epilogues) of three workgroups.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
@@ -24,6 +24,7 @@ __global__ void fill_rand(int8_t* p, size_t n, unsigned seed) {
 int main(int argc, char** argv) {
   const int OW = argc > 1 ? atoi(argv[1]) : 7;
   const int dbg = argc > 2 ? atoi(argv[2]) : 0;
+  const bool ds = argc > 3 ? atoi(argv[3]) != 0 : true;  // 0: conv1 alone (the engine's layer2.0 / layer3.0 since round 6)
   const int C = OW == 28 ? 64 : OW == 14 ? 128 : 256, OC = 2 * C, N = 256, W = 2 * OW;
   const size_t xin = (size_t)N * W * W * C, yout = (size_t)N * OW * OW * OC;
   const size_t wb = (size_t)OC * (C / 32) * 304, db = (size_t)OC * (C / 32) * 48;
@@ -41,9 +42,9 @@ int main(int argc, char** argv) {
   a.N = N; a.H = W; a.W = W; a.C = C; a.OH = OW; a.OW = OW; a.OC = OC; a.OCp = OC; a.K = 9 * C;
   a.kH = a.kW = 3; a.sH = a.sW = 2; a.pH = a.pW = 1; a.P = N * OW * OW; a.relu = 1; a.out_kind = 0; a.dbg = dbg;
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
-  for (int it = 0; it < 20; ++it) launch_conv3x3s2i(a, wd, al, be, yd, 0);
+  for (int it = 0; it < 20; ++it) launch_conv3x3s2i(a, ds ? wd : nullptr, al, be, yd, 0);
   hipEventRecord(e0, 0);
-  for (int it = 0; it < 20; ++it) launch_conv3x3s2i(a, wd, al, be, yd, 0);
+  for (int it = 0; it < 20; ++it) launch_conv3x3s2i(a, ds ? wd : nullptr, al, be, yd, 0);
   hipEventRecord(e1, 0);
   if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     printf("launch/sync failed\n");
