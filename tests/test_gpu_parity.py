@@ -237,15 +237,16 @@ def test_conv2_with_downsample_residual_rejects_bad_shapes(gpu):
 def test_resnet18_downsample_residual_matches_fused_downsample(gpu, knobs):
     """B=256 forward with the layer2.0 / layer3.0 downsample computed in conv2's
     epilogue (the default) == knob ds_split = -1 (the stride-2 launch stores
-    it, conv2 reads it)."""
+    it, conv2 reads it) == 1 / 2 (in conv2 at layer3.0 / layer2.0 only)."""
     from dlq_amd.models import ResNet18Int8, synthetic_images
     sd, scales = model_and_scales()
     x = synthetic_images(256, seed=23).cuda()
     model = ResNet18Int8(sd, scales, max_batch=256)
     split = model(x).cpu().numpy()
-    knobs("ds_split", -1)
-    fused = model(x).cpu().numpy()
-    assert np.array_equal(split.view(np.int32), fused.view(np.int32))
+    for v in (-1, 1, 2):
+        knobs("ds_split", v)
+        other = model(x).cpu().numpy()
+        assert np.array_equal(split.view(np.int32), other.view(np.int32)), f"ds_split = {v}"
 
 
 @pytest.mark.parametrize("C,H", [(128, 28), (256, 14), (512, 7)])
