@@ -396,7 +396,7 @@ def test_resnet18_fused_head_matches_split_head(gpu, knobs):
     assert np.array_equal(fused.view(np.int32), split.view(np.int32))
 
 
-@pytest.mark.parametrize("B", [3, 256])
+@pytest.mark.parametrize("B", [1, 3, 9, 256])
 def test_resnet18_pooled_last_conv_matches_fused_head(gpu, knobs, B):
     """The last conv pooling its own output (default: conv3x3i GAP, then the
     FC alone) == knob gap_epi = -1 (the fused gap_fc_kernel head), bit for
